@@ -1,0 +1,188 @@
+"""Benchmark: audio-samples/sec of filter + envelope + noise floor + peaks
+(BASELINE.json metric) on a synthetic batch of 1024 x 60 s 44.1 kHz mono int16
+recordings per GPU, inputs resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode native|reference]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One process per GPU; files are sharded (weak scaling: every rank processes its
+own 1024 recordings, no data-path collective).  After the timed steps the
+per-file peak counts are gathered to rank 0 over RCCL (the only collective).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "audio-samples/sec (filter+envelope+peaks), 1024x60s@44.1kHz batch, 1 & 8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", default="reference", choices=["reference", "native"])
+    ap.add_argument("--files", type=int, default=1024, help="recordings per GPU")
+    ap.add_argument("--secs", type=float, default=60.0)
+    ap.add_argument("--fs", type=int, default=44100)
+    ap.add_argument("--cpu-files", type=int, default=-1, help="CPU baseline sample size (-1: auto, 0: skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, channels: int = 1) -> dict:
+    """Algorithmic HBM bytes per launch of the dominant kernels."""
+    if mode == "native":
+        # every PCM sample is read once (int16), the decimated output written once
+        return {"k_envelope_native": n_files * (n_frames * channels * 2 + nd * 8)}
+    # reference: the picked int16 samples, y kept in scratch (written fwd, rewritten bwd, read twice),
+    # env written once
+    return {"k_envelope_ref": n_files * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8),
+            "k_rolling_quantile": n_files * (nd * 8 + nd * 8)}
+
+
+def cpu_baseline(mode: str, fs: int, n_frames: int, n_files: int, params: dict) -> dict:
+    """The CPU oracle (C restatement of the reference path) on a bounded sample, all host cores."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    d = O.derive(fs, params)
+    with ThreadPoolExecutor(cores) as ex:
+        pcms = list(ex.map(lambda f: O.synth(10_000 + f, n_frames, fs, 1), range(n_files)))
+
+    def one(pcm):
+        env = O.preprocess_ref(pcm, d) if mode == "reference" else O.preprocess_native(pcm, d)
+        fl, tr, _ = O.noise_floor(env, d, params)
+        return len(O.raw_peaks(env, fl, d, params))
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(one, pcms))
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n_files * n_frames / dt, "unit": "audio-samples/s", "cores": cores, "kind": "port",
+            "sample": f"{n_files} x {n_frames / fs:.0f} s {fs} Hz mono int16 synthetic recordings, {mode} mode, "
+                      f"oracle/bpmx_oracle.c on {cores} threads of {cpu}; {dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from bpm_analysis_amd import DEFAULT_PARAMS
+    from bpm_analysis_amd.design import design
+    from bpm_analysis_amd.engine import Detector
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    det = Detector(local)
+    params = dict(DEFAULT_PARAMS)
+    params["save_filtered_wav"] = False
+    fs, F = args.fs, args.files
+    n = int(round(args.secs * fs))
+    d = design(fs, params, log=False)
+    fo = np.arange(F + 1, dtype=np.int64) * n
+    pcm = det.synth(fo, fs, 1, seed0=rank * F)
+    out = det.alloc(fo, d.ds, d.sr)
+    nd = -(-n // d.ds)
+
+    def step():
+        det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    det.profile(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    det.profile(False)
+    prof = det.profile_read()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=det.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        # final result gather (RCCL): per-file raw-peak counts of every shard to rank 0
+        counts = out.n_peaks.clone()
+        gathered = [torch.empty_like(counts) for _ in range(world)] if rank == 0 else None
+        dist.gather(counts, gathered, dst=0)
+        total_peaks = int(sum(int(g.sum()) for g in gathered)) if rank == 0 else 0
+    else:
+        total_peaks = int(out.n_peaks.sum())
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        value = world * F * n / (elapsed / args.steps)
+        abytes = algorithmic_bytes(args.mode, F, n, nd)
+        timed = {k: v for k, v in prof.items() if k in abytes}
+        dom = max(timed, key=lambda k: timed[k][1]) if timed else None
+        roof = None
+        if dom:
+            cnt, tot = timed[dom]
+            avg_s = tot / cnt / 1e3
+            ach = abytes[dom] / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
+                    "kernel_avg_ms": round(avg_s * 1e3, 4)}
+        kernels = {k: {"launches": c, "avg_ms": round(t / c, 4)} for k, (c, t) in sorted(prof.items())}
+        cpu = None
+        if not args.no_cpu and args.cpu_files != 0:
+            nfc = args.cpu_files if args.cpu_files > 0 else (256 if args.mode == "reference" else 64)
+            cpu = cpu_baseline(args.mode, fs, n, nfc, params)
+        line = {
+            "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
+                                   f"(filter+envelope+noise floor+raw peaks)",
+                       "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
+                       "parallelism": f"file-sharded x{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
+            "kernels": kernels, "total_raw_peaks": total_peaks,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

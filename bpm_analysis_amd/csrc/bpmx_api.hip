@@ -1,0 +1,394 @@
+/*
+ * bpmx_api.hip — host side of the C ABI (include/bpmx.h): context, scratch,
+ * stage sequencing, synthetic input, per-kernel event timing.
+ *
+ * Stage order follows analyze_wav_file (bpm_analysis.py:1731-1732) and the
+ * classifier's raw-peak call (:89 -> :223-229):
+ *   ENVELOPE  k_envelope_ref | native kernels (k_envelope_native.hip)
+ *   FLOOR     k_block_stats, k_quantile, k_find_peaks(-env), k_interp,
+ *             k_rolling_quantile (draft), k_sanitize, k_interp,
+ *             k_rolling_quantile (final), k_floor_final
+ *   PEAKS     k_find_peaks(env, height=floor)
+ * Everything is enqueued on one stream; no host synchronisation inside a run
+ * except the (cached) upload of the batch geometry.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "bpmx_common.h"
+#include "bpmx_kernels.h"
+#include "bpmx_ctx.h"
+#include "bpmx_native.h"
+#include "bpmx_synth.h"
+
+using namespace bpmx;
+
+namespace bpmx {
+thread_local std::string g_err;
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace bpmx
+
+namespace {
+
+__global__ __launch_bounds__(64) void k_synth_beats(uint64_t seed0, int n_files, const int64_t *foff,
+                                                    const int64_t *boff, int32_t fs, int64_t *s1, int64_t *s2,
+                                                    int32_t *nb) {
+    const int f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= n_files) return;
+    const int cap = (int)(boff[f + 1] - boff[f]);
+    nb[f] = bpmx_synth_beats(seed0 + (uint64_t)f, foff[f + 1] - foff[f], fs, s1 + boff[f], s2 + boff[f], cap);
+}
+
+__global__ __launch_bounds__(256) void k_synth_pcm(uint64_t seed0, int n_files, const int64_t *foff,
+                                                   const int64_t *boff, int32_t fs, int channels,
+                                                   const int64_t *s1, const int64_t *s2, const int32_t *nb,
+                                                   int16_t *pcm) {
+    const int f = blockIdx.y;
+    const int64_t n = foff[f + 1] - foff[f];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        for (int c = 0; c < channels; ++c)
+            pcm[(foff[f] + i) * channels + c] =
+                bpmx_synth_sample(seed0 + (uint64_t)f, c, i, fs, s1 + boff[f], s2 + boff[f], nb[f]);
+}
+
+int beats_cap(int64_t n_frames, int32_t fs) {
+    int64_t q = fs / 4 > 0 ? fs / 4 : 1;
+    return (int)(n_frames / q) + 16;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bpmx_abi_version(void) { return BPMX_ABI_VERSION; }
+
+const char *bpmx_last_error(void) { return g_err.c_str(); }
+
+int bpmx_create(int device, bpmx_ctx **out) {
+    if (!out) return fail(BPMX_E_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(BPMX_E_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(BPMX_E_ARG, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(BPMX_E_NODEV, std::string("libbpmx is built for gfx950, device is ") + prop.gcnArchName);
+    bpmx_ctx *c = new bpmx_ctx();
+    c->device = device;
+    *out = c;
+    return BPMX_OK;
+}
+
+void bpmx_destroy(bpmx_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (auto &kv : ctx->bufs)
+        if (kv.second.first) (void)hipFree(kv.second.first);
+    for (auto &r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : ctx->pool) (void)hipEventDestroy(e);
+    delete ctx;
+}
+
+int64_t bpmx_decimated_length(int64_t n_frames, int32_t ds) {
+    if (ds < 1) ds = 1;
+    return n_frames <= 0 ? 0 : (n_frames + ds - 1) / ds;
+}
+
+void bpmx_synth_host(uint64_t seed, int64_t n_frames, int32_t fs, int32_t channels, int16_t *out) {
+    const int cap = beats_cap(n_frames, fs);
+    std::vector<int64_t> s1(cap), s2(cap);
+    const int nb = bpmx_synth_beats(seed, n_frames, fs, s1.data(), s2.data(), cap);
+    for (int64_t i = 0; i < n_frames; ++i)
+        for (int c = 0; c < channels; ++c)
+            out[i * channels + c] = bpmx_synth_sample(seed, c, i, fs, s1.data(), s2.data(), nb);
+}
+
+int bpmx_synth(bpmx_ctx *ctx, uint64_t seed0, int32_t n_files, const int64_t *frame_offsets, int32_t fs,
+               int32_t channels, int16_t *pcm, void *stream) {
+    if (!ctx || !frame_offsets || !pcm || n_files < 1 || fs < 4 || channels < 1)
+        return fail(BPMX_E_ARG, "bpmx_synth: bad argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<int64_t> geo(2 * (n_files + 1));
+    int64_t acc = 0, maxn = 0;
+    for (int f = 0; f <= n_files; ++f) {
+        geo[f] = frame_offsets[f] - frame_offsets[0];
+        if (f < n_files) {
+            int64_t n = frame_offsets[f + 1] - frame_offsets[f];
+            if (n < 0) return fail(BPMX_E_ARG, "bpmx_synth: frame offsets must be non-decreasing");
+            geo[n_files + 1 + f] = acc;
+            acc += beats_cap(n, fs);
+            maxn = std::max(maxn, n);
+        }
+    }
+    geo[n_files + 1 + n_files] = acc;
+    int rc = BPMX_OK;
+    int64_t *dgeo = (int64_t *)ctx->buf("synth_geo", geo.size() * 8, &rc);
+    int64_t *s1 = (int64_t *)ctx->buf("synth_s1", (size_t)acc * 8, &rc);
+    int64_t *s2 = (int64_t *)ctx->buf("synth_s2", (size_t)acc * 8, &rc);
+    int32_t *nb = (int32_t *)ctx->buf("synth_nb", (size_t)n_files * 4, &rc);
+    if (rc != BPMX_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(dgeo, geo.data(), geo.size() * 8, hipMemcpyHostToDevice, s));
+    const int64_t *foff = dgeo, *boff = dgeo + n_files + 1;
+    int16_t *base = pcm + frame_offsets[0] * channels;
+    LAUNCH(ctx, s, "k_synth_beats", k_synth_beats, dim3((n_files + 63) / 64), dim3(64), 0, s, seed0, n_files, foff,
+           boff, fs, s1, s2, nb);
+    int gx = (int)std::min<int64_t>((maxn + 255) / 256, 512);
+    LAUNCH(ctx, s, "k_synth_pcm", k_synth_pcm, dim3(std::max(gx, 1), n_files), dim3(256), 0, s, seed0, n_files,
+           foff, boff, fs, channels, s1, s2, nb, base);
+    return BPMX_OK;
+}
+
+int bpmx_profile(bpmx_ctx *ctx, int on) {
+    if (!ctx) return fail(BPMX_E_ARG, "ctx is NULL");
+    ctx->prof = on != 0;
+    if (on) ctx->totals.clear();
+    return BPMX_OK;
+}
+
+int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len) {
+    if (!ctx) return fail(BPMX_E_ARG, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    for (auto &r : ctx->recs) {
+        HIP_TRY(hipEventSynchronize(r.b));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        auto &t = ctx->totals[r.name];
+        t.first += 1;
+        t.second += ms;
+        ctx->pool.push_back(r.a);
+        ctx->pool.push_back(r.b);
+    }
+    ctx->recs.clear();
+    std::string s;
+    char line[256];
+    for (auto &kv : ctx->totals) {
+        std::snprintf(line, sizeof line, "%s %ld %.6f\n", kv.first.c_str(), kv.second.first, kv.second.second);
+        s += line;
+    }
+    if (buf && len > 0) {
+        std::strncpy(buf, s.c_str(), (size_t)len - 1);
+        buf[len - 1] = 0;
+    }
+    return (int)s.size();
+}
+
+int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {
+    if (!ctx || !P || !B || !O) return fail(BPMX_E_ARG, "NULL argument");
+    const int F = B->n_files;
+    if (F < 1 || !B->frame_offsets) return fail(BPMX_E_ARG, "empty batch");
+    if (P->mode != BPMX_MODE_REFERENCE && P->mode != BPMX_MODE_NATIVE) return fail(BPMX_E_ARG, "bad mode");
+    if (P->dtype < BPMX_DT_U8 || P->dtype > BPMX_DT_F64) return fail(BPMX_E_ARG, "bad dtype");
+    if (P->channels < 1 || P->ds < 1 || P->sr < 1) return fail(BPMX_E_ARG, "bad channels/ds/sr");
+    const int st = P->stages;
+    if (st <= 0 || st > BPMX_STAGE_ALL) return fail(BPMX_E_ARG, "bad stage mask");
+    const bool do_env = st & BPMX_STAGE_ENVELOPE, do_floor = st & BPMX_STAGE_FLOOR, do_peaks = st & BPMX_STAGE_PEAKS;
+    if (do_env && !B->pcm) return fail(BPMX_E_ARG, "ENVELOPE stage needs pcm");
+    if (!O->env || !O->n_troughs || !O->n_peaks || !O->flags) return fail(BPMX_E_ARG, "missing output arrays");
+    if ((do_floor || do_peaks) && !O->floor) return fail(BPMX_E_ARG, "floor array required");
+    if (do_floor && !O->troughs) return fail(BPMX_E_ARG, "troughs array required");
+    if (do_peaks && !O->peaks) return fail(BPMX_E_ARG, "peaks array required");
+    if ((do_floor || do_peaks) && P->distance < 1) return fail(BPMX_E_ARG, "`distance` must be greater or equal to 1");
+    if (do_floor && (P->noise_window < P->min_periods || P->min_periods < 1))
+        return fail(BPMX_E_ARG, "min_periods must be <= noise window");
+    if (do_env && P->env_window < 1) return fail(BPMX_E_ARG, "envelope window must be >= 1");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+
+    /* ---- geometry ---- */
+    std::vector<int64_t> foff(F + 1), doff(F + 1), boff(F + 1);
+    std::vector<int32_t> active(F), flags0(F);
+    int64_t maxnd = 0;
+    foff[0] = 0; doff[0] = 0; boff[0] = 0;
+    for (int f = 0; f < F; ++f) {
+        const int64_t n = B->frame_offsets[f + 1] - B->frame_offsets[f];
+        if (n < 0) return fail(BPMX_E_ARG, "frame offsets must be non-decreasing");
+        const int64_t nd = bpmx_decimated_length(n, P->ds);
+        foff[f + 1] = foff[f] + n;
+        doff[f + 1] = doff[f] + nd;
+        boff[f + 1] = boff[f] + (nd + 63) / 64;
+        maxnd = std::max(maxnd, nd);
+        const bool ok = do_env ? nd > 15 : nd >= 1;
+        active[f] = ok ? 1 : 0;
+        flags0[f] = ok ? 0 : BPMX_F_TOO_SHORT;
+        if (nd >= (int64_t)INT_MAX / 2) return fail(BPMX_E_LIMIT, "recording too long");
+    }
+    const int64_t sumnd = doff[F], sumb = boff[F];
+    if (sumnd == 0) return fail(BPMX_E_ARG, "empty recordings");
+
+    int rc = BPMX_OK;
+    std::vector<int64_t> geo;
+    geo.reserve(3 * (F + 1));
+    geo.insert(geo.end(), foff.begin(), foff.end());
+    geo.insert(geo.end(), doff.begin(), doff.end());
+    geo.insert(geo.end(), boff.begin(), boff.end());
+    int64_t *dgeo = (int64_t *)ctx->buf("geo", geo.size() * 8, &rc);
+    int32_t *di = (int32_t *)ctx->buf("geo_i", (size_t)F * 4 * 8, &rc);
+    if (rc != BPMX_OK) return rc;
+    std::vector<int64_t> key = geo;
+    key.push_back(F);
+    key.push_back(do_env);
+    if (key != ctx->g_key) {
+        HIP_TRY(hipMemcpyAsync(dgeo, geo.data(), geo.size() * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(di, active.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->g_key = key;
+    }
+    const int64_t *d_foff = dgeo, *d_doff = dgeo + F + 1, *d_boff = dgeo + 2 * (F + 1);
+    const int32_t *d_active = di;
+    int32_t *d_run1 = di + F, *d_run2 = di + 2 * F, *d_an1 = di + 3 * F, *d_an2 = di + 4 * F, *d_nraw = di + 5 * F;
+
+    HIP_TRY(hipMemcpyAsync(O->flags, flags0.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+    if (do_floor) HIP_TRY(hipMemsetAsync(O->n_troughs, 0, (size_t)F * 4, s));
+    if (do_peaks) HIP_TRY(hipMemsetAsync(O->n_peaks, 0, (size_t)F * 4, s));
+    HIP_TRY(hipMemsetAsync(d_run1, 0, (size_t)F * 4 * 5, s));
+
+    /* ---- ENVELOPE ---- */
+    if (do_env) {
+        if (P->mode == BPMX_MODE_REFERENCE) {
+            double *scr = (double *)ctx->buf("ref_scratch", (size_t)(maxnd + 30) * F * 8, &rc);
+            if (rc != BPMX_OK) return rc;
+            EnvRefArgs a;
+            a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.active = d_active;
+            a.n_files = F; a.dtype = P->dtype; a.channels = P->channels; a.ds = P->ds; a.env_window = P->env_window;
+            std::memcpy(a.b, P->ba_b, sizeof a.b);
+            std::memcpy(a.a, P->ba_a, sizeof a.a);
+            std::memcpy(a.zi, P->ba_zi, sizeof a.zi);
+            a.scratch = scr; a.env = O->env; a.y = O->y;
+            LAUNCH(ctx, s, "k_envelope_ref", k_envelope_ref, dim3((F + 63) / 64), dim3(64), 0, s, a);
+        } else {
+            int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
+            if (r != BPMX_OK) return r;
+        }
+    }
+    if (!do_floor && !do_peaks) return BPMX_OK;
+
+    /* ---- shared detection inputs: block tables, quantiles ---- */
+    double *bmax = (double *)ctx->buf("bmax", (size_t)sumb * 8, &rc);
+    double *bmin = (double *)ctx->buf("bmin", (size_t)sumb * 8, &rc);
+    double *qv = (double *)ctx->buf("qv", (size_t)F * Q_SLOTS * 8, &rc);
+    int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
+    uint8_t *state = (uint8_t *)ctx->buf("state", (size_t)sumnd, &rc);
+    if (rc != BPMX_OK) return rc;
+    {
+        BlockStatArgs a;
+        a.env = O->env; a.doff = d_doff; a.boff = d_boff; a.active = d_active; a.n_files = F;
+        a.bmax = bmax; a.bmin = bmin;
+        LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F), dim3(256), 0, s, a);
+    }
+    {
+        QuantArgs a;
+        a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv;
+        int L = 0;
+        auto add = [&](double q, int slot) {
+            for (int l = 0; l < L; ++l)
+                if (a.q[l] == q && a.slot[l] == slot) return;
+            a.q[L] = q; a.slot[L] = slot; ++L;
+        };
+        if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->noise_floor_q, Q_NOISE); add(P->fallback_q, Q_FALLBACK); }
+        if (do_peaks) add(P->peak_prom_q, Q_PEAK);
+        a.n_levels = L;
+        LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(256), 0, s, a);
+    }
+
+    /* ---- FLOOR ---- */
+    if (do_floor) {
+        int64_t *rawt = (int64_t *)ctx->buf("raw_troughs", (size_t)sumnd * 8, &rc);
+        double *dense = (double *)ctx->buf("dense", (size_t)sumnd * 8, &rc);
+        double *draft = (double *)ctx->buf("draft", (size_t)sumnd * 8, &rc);
+        if (rc != BPMX_OK) return rc;
+        {
+            PeakArgs a;
+            a.env = O->env; a.height = nullptr; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
+            a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
+            a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
+            a.run_out = d_run1; a.run_min = 5;
+            LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+        }
+        /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
+        const int64_t W = P->noise_window;
+        int T = 256;
+        int cap = (int)((W + T + 64 + 63) / 64 * 64);
+        size_t lds = rollq_lds_bytes(T, cap);
+        if (lds > 80 * 1024) {
+            T = 128;
+            cap = (int)((W + T + 64 + 63) / 64 * 64);
+            lds = rollq_lds_bytes(T, cap);
+        }
+        if (lds > 160 * 1024 || W + T >= 65000)
+            return fail(BPMX_E_LIMIT, "noise window of " + std::to_string(W) +
+                                          " samples exceeds the LDS rolling-quantile kernel (max ~6000)");
+        auto rollq = [&](const int32_t *run, const int64_t *tr, double *outp, int32_t *allnan) -> int {
+            RollqArgs a;
+            a.dense = dense; a.doff = d_doff; a.troughs = tr; a.run = run; a.n_files = F;
+            a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
+            a.out = outp; a.allnan = allnan;
+            if (T == 256) {
+                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<256>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_rolling_quantile", k_rolling_quantile<256>, dim3(F), dim3(256), lds, s, a);
+            } else {
+                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<128>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_rolling_quantile", k_rolling_quantile<128>, dim3(F), dim3(128), lds, s, a);
+            }
+            return BPMX_OK;
+        };
+        const dim3 g2((unsigned)((maxnd + 255) / 256), F);
+        if (O->n_raw_troughs)
+            HIP_TRY(hipMemcpyAsync(O->n_raw_troughs, d_nraw, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
+        {
+            InterpArgs a;
+            a.env = O->env; a.doff = d_doff; a.troughs = rawt; a.ntr = d_nraw; a.run = d_run1; a.n_files = F;
+            a.dense = dense;
+            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
+        }
+        if ((rc = rollq(d_run1, rawt, draft, d_an1)) != BPMX_OK) return rc;
+        {
+            SanitizeArgs a;
+            a.env = O->env; a.draft = draft; a.doff = d_doff; a.active = d_active; a.raw = rawt; a.nraw = d_nraw;
+            a.n_files = F; a.mult = P->reject_mult; a.out = O->troughs; a.nout = O->n_troughs; a.flags = O->flags;
+            a.run2 = d_run2;
+            LAUNCH(ctx, s, "k_sanitize", k_sanitize, dim3(F), dim3(256), 0, s, a);
+        }
+        {
+            InterpArgs a;
+            a.env = O->env; a.doff = d_doff; a.troughs = O->troughs; a.ntr = O->n_troughs; a.run = d_run2;
+            a.n_files = F; a.dense = dense;
+            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
+        }
+        if ((rc = rollq(d_run2, O->troughs, O->floor, d_an2)) != BPMX_OK) return rc;
+        {
+            FinalArgs a;
+            a.draft = draft; a.doff = d_doff; a.active = d_active; a.qv = qv; a.allnan_draft = d_an1;
+            a.allnan_final = d_an2; a.n_files = F; a.floor = O->floor; a.flags = O->flags;
+            LAUNCH(ctx, s, "k_floor_final", k_floor_final, g2, dim3(256), 0, s, a);
+        }
+    }
+
+    /* ---- PEAKS ---- */
+    if (do_peaks) {
+        PeakArgs a;
+        a.env = O->env; a.height = O->floor; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
+        a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
+        a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
+        a.run_out = nullptr; a.run_min = 0;
+        LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+    }
+    return BPMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,156 @@
+/*
+ * bpmx_common.h — device helpers shared by the bpmx kernels (gfx950, wave64).
+ *
+ * Everything here is compiled with -ffp-contract=off: the bit-exact stages
+ * must evaluate a*b+c as a rounded product followed by a rounded sum, as the
+ * reference's compiled scipy/pandas/numpy loops do.  Kernels that may fuse
+ * call __builtin_fma explicitly.
+ */
+#ifndef BPMX_COMMON_H
+#define BPMX_COMMON_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bpmx.h"
+
+#define BPMX_WAVE 64
+
+namespace bpmx {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+/* ---- PCM access ------------------------------------------------------- */
+/* numpy dtype of x after `np.mean(axis=1)` (bpm_analysis.py:1015-1016):
+ * mono keeps its dtype, multi-channel ints -> f64, f32 -> f32. */
+__host__ __device__ __forceinline__ int work_dtype(int dtype, int channels) {
+    if (channels <= 1) return dtype;
+    return dtype == BPMX_DT_F32 ? BPMX_DT_F32 : BPMX_DT_F64;
+}
+
+__device__ __forceinline__ double load_pcm(const void *pcm, int dtype, int64_t idx) {
+    switch (dtype) {
+    case BPMX_DT_U8: return (double)((const uint8_t *)pcm)[idx];
+    case BPMX_DT_I16: return (double)((const int16_t *)pcm)[idx];
+    case BPMX_DT_I32: return (double)((const int32_t *)pcm)[idx];
+    case BPMX_DT_F32: return (double)((const float *)pcm)[idx];
+    default: return ((const double *)pcm)[idx];
+    }
+}
+
+/* value of frame `frame` after the channel mean */
+__device__ __forceinline__ double frame_value(const void *pcm, int dtype, int channels, int64_t frame) {
+    if (channels <= 1) return load_pcm(pcm, dtype, frame);
+    if (dtype == BPMX_DT_F32) {
+        const float *p = (const float *)pcm + frame * channels;
+        float s = p[0];
+        for (int c = 1; c < channels; ++c) s = s + p[c];
+        return (double)(s / (float)channels);
+    }
+    double s = load_pcm(pcm, dtype, frame * channels);
+    for (int c = 1; c < channels; ++c) s = s + load_pcm(pcm, dtype, frame * channels + c);
+    return s / (double)channels;
+}
+
+/* scipy odd_ext (_arraytools.py:57-107): 2*end - v evaluated in the working
+ * dtype, i.e. with integer wraparound or float32 rounding. */
+__device__ __forceinline__ double odd_ext(int wdt, double end, double v) {
+    switch (wdt) {
+    case BPMX_DT_U8: return (double)(uint8_t)(uint32_t)(2 * (int64_t)end - (int64_t)v);
+    case BPMX_DT_I16: return (double)(int16_t)(uint16_t)(uint32_t)(2 * (int64_t)end - (int64_t)v);
+    case BPMX_DT_I32: return (double)(int32_t)(uint32_t)(2 * (int64_t)end - (int64_t)v);
+    case BPMX_DT_F32: {
+        float t = (float)end * 2.0f;
+        return (double)(t - (float)v);
+    }
+    default: return 2.0 * end - v;
+    }
+}
+
+/* ---- order-preserving f64 key ----------------------------------------- */
+__device__ __forceinline__ uint64_t f64_key(double v) {
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_f64(uint64_t k) {
+    uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+/* numpy _lerp (numpy/lib/_function_base_impl.py:4639-4660) */
+__host__ __device__ __forceinline__ double np_lerp(double a, double b, double t) {
+    double d = b - a;
+    if (t >= 0.5) return b - d * (1.0 - t);
+    return a + d * t;
+}
+
+/* pandas centered fixed window (pandas/core/indexers/objects.py:93-120) */
+__host__ __device__ __forceinline__ void win_bounds(int64_t i, int64_t n, int64_t w, int64_t &s, int64_t &e) {
+    int64_t off = (w - 1) / 2;
+    int64_t ee = i + 1 + off, ss = ee - w;
+    e = ee < 0 ? 0 : (ee > n ? n : ee);
+    s = ss < 0 ? 0 : (ss > n ? n : ss);
+}
+
+/* ---- wave / block primitives (64-lane) -------------------------------- */
+__device__ __forceinline__ double wave_min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+/* exclusive block scan of 0/1 flags; `sh` holds NT/64+1 ints.  Returns the
+ * exclusive prefix, writes the block total to *total.  Ends with a barrier. */
+template <int NT>
+__device__ __forceinline__ int block_scan_flag(bool flag, int *sh, int *total) {
+    const int lane = lane_id(), wid = wave_id();
+    unsigned long long m = __ballot(flag);
+    int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) sh[wid] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int w = 0; w < NT / 64; ++w) { int t = sh[w]; sh[w] = acc; acc += t; }
+        sh[NT / 64] = acc;
+    }
+    __syncthreads();
+    int r = pre + sh[wid];
+    *total = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+/* exclusive block scan of small non-negative ints */
+template <int NT>
+__device__ __forceinline__ int block_scan_int(int v, int *sh, int *total) {
+    const int lane = lane_id(), wid = wave_id();
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int w = 0; w < NT / 64; ++w) { int t = sh[w]; sh[w] = acc; acc += t; }
+        sh[NT / 64] = acc;
+    }
+    __syncthreads();
+    int r = x - v + sh[wid];
+    *total = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+}  // namespace bpmx
+
+#endif

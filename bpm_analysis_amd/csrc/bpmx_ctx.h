@@ -1,0 +1,94 @@
+/*
+ * bpmx_ctx.h — host-side context shared by the bpmx translation units.
+ */
+#ifndef BPMX_CTX_H
+#define BPMX_CTX_H
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/bpmx.h"
+
+namespace bpmx {
+int fail(int code, const std::string &msg);
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return bpmx::fail(BPMX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct bpmx_ctx {
+    int device = 0;
+    std::map<std::string, std::pair<void *, size_t>> bufs;
+    std::vector<int64_t> g_key;   /* geometry of the last upload */
+    bool prof = false;
+    struct Rec { std::string name; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    std::map<std::string, std::pair<long, double>> totals;
+
+    /* grow-only device scratch */
+    void *buf(const std::string &name, size_t bytes, int *rc) {
+        auto &e = bufs[name];
+        if (e.second < bytes) {
+            if (e.first) (void)hipFree(e.first);
+            e.first = nullptr;
+            e.second = 0;
+            size_t want = bytes + bytes / 8 + 256;
+            if (hipMalloc(&e.first, want) != hipSuccess) {
+                e.first = nullptr;
+                *rc = bpmx::fail(BPMX_E_HIP, "hipMalloc failed for scratch '" + name + "' (" + std::to_string(want) + " B)");
+                return nullptr;
+            }
+            e.second = want;
+        }
+        return e.first;
+    }
+    hipEvent_t ev() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+
+namespace bpmx {
+
+/* one kernel launch, optionally bracketed by events for bpmx_profile */
+struct Launch {
+    bpmx_ctx *ctx;
+    hipStream_t s;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    Launch(bpmx_ctx *c, hipStream_t st, const char *n) : ctx(c), s(st), name(n) {
+        if (ctx->prof) { a = ctx->ev(); (void)hipEventRecord(a, s); }
+    }
+    int done() {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(BPMX_E_HIP, std::string("launch of ") + name + ": " + hipGetErrorString(e));
+        if (ctx->prof) {
+            b = ctx->ev();
+            (void)hipEventRecord(b, s);
+            ctx->recs.push_back({name, a, b});
+        }
+        return BPMX_OK;
+    }
+};
+
+}  // namespace bpmx
+
+#define LAUNCH(ctx, stream, name, ...)                \
+    do {                                              \
+        bpmx::Launch _l(ctx, stream, name);           \
+        hipLaunchKernelGGL(__VA_ARGS__);              \
+        int _rc = _l.done();                          \
+        if (_rc != BPMX_OK) return _rc;               \
+    } while (0)
+
+#endif

@@ -1,0 +1,130 @@
+/*
+ * bpmx_kernels.h — kernel argument blocks and launch declarations.
+ */
+#ifndef BPMX_KERNELS_H
+#define BPMX_KERNELS_H
+
+#include "bpmx_common.h"
+
+namespace bpmx {
+
+/* per-file quantile slots in the qv[F][4] table */
+enum { Q_TROUGH = 0, Q_PEAK = 1, Q_NOISE = 2, Q_FALLBACK = 3, Q_SLOTS = 4 };
+
+struct EnvRefArgs {
+    const void *pcm;
+    const int64_t *foff;   /* [F+1] frame offsets */
+    const int64_t *doff;   /* [F+1] decimated offsets */
+    const int32_t *active; /* [F] */
+    int32_t n_files, dtype, channels, ds, env_window;
+    double b[5], a[5], zi[4];
+    double *scratch;       /* interleaved [(maxNd+30) * F] */
+    double *env;           /* [sumNd] */
+    double *y;             /* [sumNd] or null */
+};
+
+struct QuantArgs {
+    const double *env;
+    const int64_t *doff;
+    const int32_t *active;
+    int32_t n_files, n_levels;
+    int32_t slot[Q_SLOTS];  /* qv slot written by level l */
+    double q[Q_SLOTS];
+    double *qv;             /* [F][Q_SLOTS] */
+};
+
+struct BlockStatArgs {
+    const double *env;
+    const int64_t *doff;
+    const int64_t *boff;   /* [F+1] offsets of 64-sample block tables */
+    const int32_t *active;
+    int32_t n_files;
+    double *bmax, *bmin;
+};
+
+struct PeakArgs {
+    const double *env;
+    const double *height;  /* per-sample minimum height or null (same indexing as env) */
+    const int64_t *doff, *boff;
+    const int32_t *active;
+    const double *bmax, *bmin;
+    const double *qv;
+    int32_t qslot;
+    int32_t n_files;
+    int32_t distance;
+    double sign;           /* +1: find_peaks(env), -1: find_peaks(-env) */
+    int32_t *cand;         /* scratch [sumNd] */
+    uint8_t *state;        /* scratch [sumNd] */
+    int64_t *out;          /* [sumNd] */
+    int32_t *nout;         /* [F] */
+    int32_t *run_out;      /* optional [F]: 1 if nout >= run_min */
+    int32_t run_min;
+};
+
+struct InterpArgs {
+    const double *env;
+    const int64_t *doff;
+    const int64_t *troughs;  /* per-file slices at doff */
+    const int32_t *ntr;
+    const int32_t *run;      /* [F] files to process */
+    int32_t n_files;
+    double *dense;
+};
+
+struct RollqArgs {
+    const double *dense;
+    const int64_t *doff;
+    const int64_t *troughs;  /* first trough = first non-NaN dense sample */
+    const int32_t *run;
+    int32_t n_files, window, min_periods, cap;
+    double q;
+    double *out;
+    int32_t *allnan;         /* [F] */
+};
+
+struct SanitizeArgs {
+    const double *env, *draft;
+    const int64_t *doff;
+    const int32_t *active;
+    const int64_t *raw;      /* raw troughs (slices at doff) */
+    const int32_t *nraw;
+    int32_t n_files;
+    double mult;
+    int64_t *out;
+    int32_t *nout;
+    int32_t *flags;
+    int32_t *run2;           /* [F] files that need the second floor pass */
+};
+
+struct FinalArgs {
+    const double *draft;
+    const int64_t *doff;
+    const int32_t *active;
+    const double *qv;
+    const int32_t *allnan_draft, *allnan_final;
+    int32_t n_files;
+    double *floor;
+    int32_t *flags;
+};
+
+/* dynamic LDS bytes of k_rolling_quantile<T> for a union capacity `cap`
+ * (multiple of 64): Av,Bv f64[cap]; nv,nsv f64[T]; ebits u64[cap/64+2];
+ * Ap,Bp u16[cap]; rem u16[cap+4]; nsp u16[T+4]; scan scratch int[64]. */
+__host__ __device__ inline size_t rollq_lds_bytes(int T, int cap) {
+    return (size_t)cap * 16 + (size_t)T * 16 + ((size_t)cap / 64 + 2) * 8 + (size_t)cap * 4 + ((size_t)cap + 4) * 2 +
+           ((size_t)T + 4) * 2 + 64 * 4;
+}
+
+__global__ void k_envelope_ref(EnvRefArgs A);
+__global__ void k_quantile(QuantArgs A);
+__global__ void k_block_stats(BlockStatArgs A);
+__global__ void k_find_peaks(PeakArgs A);
+__global__ void k_interp(InterpArgs A);
+__global__ void k_sanitize(SanitizeArgs A);
+__global__ void k_floor_final(FinalArgs A);
+template <int T>
+__global__ void k_rolling_quantile(RollqArgs A);
+
+}  // namespace bpmx
+
+#endif

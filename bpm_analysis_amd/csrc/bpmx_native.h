@@ -1,0 +1,17 @@
+/*
+ * bpmx_native.h — native-mode (north_star ordering) envelope entry point.
+ */
+#ifndef BPMX_NATIVE_H
+#define BPMX_NATIVE_H
+
+#include <vector>
+
+#include "bpmx_ctx.h"
+
+namespace bpmx {
+int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
+                    int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
+                    const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active);
+}
+
+#endif

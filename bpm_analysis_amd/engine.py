@@ -1,0 +1,248 @@
+"""Batch engine: device buffers (torch), the C-ABI call, per-file results.
+
+PyTorch is used here only as plumbing — device memory, streams and copies.
+All arithmetic runs in libbpmx.so's HIP kernels.
+
+A batch is a set of recordings with one sample rate, sample format and
+channel count (the reference processes one WAV at a time: gui.py:202-251; a
+batch is the MI355X unit of work).  Lengths may be ragged.  Recordings are
+laid out back to back in HBM; results use the decimated offsets
+``doff[f] = sum(Nd[:f])``.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .design import Design, design, detect_design, dtype_code, make_params
+
+MODES = {"reference": N.MODE_REFERENCE, "native": N.MODE_NATIVE}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+_TORCH_DT = None
+
+
+def torch_dtype(np_dtype):
+    global _TORCH_DT
+    torch = _torch()
+    if _TORCH_DT is None:
+        _TORCH_DT = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int16): torch.int16,
+                     np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32,
+                     np.dtype(np.float64): torch.float64}
+    return _TORCH_DT[np.dtype(np_dtype)]
+
+
+@dataclass
+class Result:
+    """Device-resident outputs of one batch (torch tensors on the GPU)."""
+    sr: int
+    ds: int
+    frame_offsets: np.ndarray      # host int64 [F+1]
+    doff: np.ndarray               # host int64 [F+1] decimated offsets
+    env: "object"
+    floor: "object"
+    y: "object"
+    troughs: "object"
+    peaks: "object"
+    n_troughs: "object"
+    n_peaks: "object"
+    n_raw_troughs: "object"
+    flags: "object"
+
+    @property
+    def n_files(self) -> int:
+        return len(self.doff) - 1
+
+    def to_host(self) -> List[dict]:
+        """Per-file numpy views after one D2H copy of each array."""
+        env = self.env.cpu().numpy()
+        floor = self.floor.cpu().numpy() if self.floor is not None else None
+        y = self.y.cpu().numpy() if self.y is not None else None
+        tr = self.troughs.cpu().numpy() if self.troughs is not None else None
+        pk = self.peaks.cpu().numpy() if self.peaks is not None else None
+        ntr = self.n_troughs.cpu().numpy()
+        npk = self.n_peaks.cpu().numpy()
+        nraw = self.n_raw_troughs.cpu().numpy()
+        flags = self.flags.cpu().numpy()
+        out = []
+        for f in range(self.n_files):
+            a, b = int(self.doff[f]), int(self.doff[f + 1])
+            out.append(dict(
+                sr=self.sr, env=env[a:b], floor=None if floor is None else floor[a:b],
+                y=None if y is None else y[a:b],
+                troughs=None if tr is None else tr[a:a + int(ntr[f])].copy(),
+                peaks=None if pk is None else pk[a:a + int(npk[f])].copy(),
+                n_raw_troughs=int(nraw[f]), flags=int(flags[f])))
+        return out
+
+
+class Detector:
+    """One libbpmx context on one GPU.  Not shared across threads without the lock."""
+
+    def __init__(self, device: int = 0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise N.BpmxError("no GPU visible to torch: the bpmx path runs only on an MI355X (gfx950)")
+        self.L = N.load()
+        self.device = torch.device("cuda", device)
+        torch.cuda.set_device(self.device)
+        torch.empty(1, device=self.device)      # initialise the HIP runtime on this device
+        ctx = ctypes.c_void_p()
+        N.check(self.L.bpmx_create(device, ctypes.byref(ctx)), "bpmx_create")
+        self.ctx = ctx
+        self.lock = threading.Lock()
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.bpmx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ #
+    def stream_handle(self) -> ctypes.c_void_p:
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def alloc(self, frame_offsets: Sequence[int], ds: int, sr: int, want_y: bool = False,
+              want_floor: bool = True, want_troughs: bool = True, want_peaks: bool = True) -> Result:
+        torch = _torch()
+        fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
+        lens = np.diff(fo)
+        nd = np.where(lens > 0, (lens + ds - 1) // ds, 0)
+        doff = np.zeros(len(fo), dtype=np.int64)
+        doff[1:] = np.cumsum(nd)
+        tot, F = int(doff[-1]), len(fo) - 1
+        dev = self.device
+        e = lambda dt: torch.empty(max(tot, 1), dtype=dt, device=dev)
+        return Result(sr=sr, ds=ds, frame_offsets=fo, doff=doff, env=e(torch.float64),
+                      floor=e(torch.float64) if want_floor else None, y=e(torch.float64) if want_y else None,
+                      troughs=e(torch.int64) if want_troughs else None, peaks=e(torch.int64) if want_peaks else None,
+                      n_troughs=torch.zeros(F, dtype=torch.int32, device=dev),
+                      n_peaks=torch.zeros(F, dtype=torch.int32, device=dev),
+                      n_raw_troughs=torch.zeros(F, dtype=torch.int32, device=dev),
+                      flags=torch.zeros(F, dtype=torch.int32, device=dev))
+
+    def run(self, pcm, frame_offsets: Sequence[int], fs: int, params: dict, mode: str = "reference",
+            stages: int = N.STAGE_ALL, channels: int = 1, out: Optional[Result] = None, want_y: bool = False,
+            d: Optional[Design] = None, log: bool = False) -> Result:
+        """Run `stages` over a device batch.  `pcm` is a CUDA tensor (or None when
+        ENVELOPE is not requested and `out.env` already holds the envelopes)."""
+        if d is None:
+            d = design(fs, params, log=log)
+        fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
+        if out is None:
+            out = self.alloc(fo, d.ds, d.sr, want_y=want_y)
+        if pcm is not None:
+            np_dt = {v: k for k, v in _torch_np_map().items()}[pcm.dtype]
+            dt = dtype_code(np_dt)
+            assert pcm.is_cuda and pcm.is_contiguous()
+            assert pcm.numel() >= int(fo[-1]) * channels, "pcm shorter than frame_offsets[-1] * channels"
+            pcm_ptr = pcm.data_ptr()
+        else:
+            dt, pcm_ptr = N.DT_I16, None
+        p = make_params(d, params, MODES[mode], stages, dt, channels)
+        b = N.Batch()
+        b.n_files = len(fo) - 1
+        b.pcm = pcm_ptr
+        b.frame_offsets = fo.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+        o = N.Out()
+        ptr = lambda t: None if t is None else t.data_ptr()
+        o.env, o.floor, o.y = ptr(out.env), ptr(out.floor), ptr(out.y)
+        o.troughs, o.peaks = ptr(out.troughs), ptr(out.peaks)
+        o.n_troughs, o.n_peaks, o.flags = ptr(out.n_troughs), ptr(out.n_peaks), ptr(out.flags)
+        o.n_raw_troughs = ptr(out.n_raw_troughs)
+        with self.lock:
+            N.check(self.L.bpmx_run(self.ctx, ctypes.byref(p), ctypes.byref(b), ctypes.byref(o),
+                                    self.stream_handle()), "bpmx_run")
+        return out
+
+    def synth(self, frame_offsets: Sequence[int], fs: int, channels: int = 1, seed0: int = 0):
+        """Synthetic int16 batch generated in HBM (bit-identical to bpmx_synth_host)."""
+        torch = _torch()
+        fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
+        pcm = torch.empty(int(fo[-1]) * channels, dtype=torch.int16, device=self.device)
+        with self.lock:
+            N.check(self.L.bpmx_synth(self.ctx, seed0, len(fo) - 1, fo.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                      fs, channels, ctypes.c_void_p(pcm.data_ptr()), self.stream_handle()),
+                    "bpmx_synth")
+        return pcm
+
+    def profile(self, on: bool):
+        N.check(self.L.bpmx_profile(self.ctx, 1 if on else 0), "bpmx_profile")
+
+    def profile_read(self) -> dict:
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = self.L.bpmx_profile_read(self.ctx, buf, len(buf))
+        if n < 0:
+            N.check(n, "bpmx_profile_read")
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, cnt, ms = line.rsplit(" ", 2)
+            out[name] = (int(cnt), float(ms))
+        return out
+
+    # ------------------------------------------------------------------ #
+    def run_host(self, recordings: List[np.ndarray], fs: int, params: dict, mode: str = "reference",
+                 stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False) -> List[dict]:
+        """Host arrays in, per-file host results out (H2D + run + D2H)."""
+        torch = _torch()
+        if not recordings:
+            return []
+        dt = recordings[0].dtype
+        ch = 1 if recordings[0].ndim == 1 else recordings[0].shape[1]
+        for r in recordings:
+            if r.dtype != dt or (1 if r.ndim == 1 else r.shape[1]) != ch:
+                raise ValueError("a batch needs one sample format and channel count")
+        fo = np.zeros(len(recordings) + 1, dtype=np.int64)
+        fo[1:] = np.cumsum([r.shape[0] for r in recordings])
+        host = np.concatenate([np.ascontiguousarray(r).reshape(-1) for r in recordings])
+        pcm = torch.from_numpy(host).to(self.device)
+        res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log)
+        torch.cuda.synchronize(self.device)
+        return res.to_host()
+
+    def run_env_host(self, envs: List[np.ndarray], sr: int, params: dict, stages: int,
+                     floors: Optional[List[np.ndarray]] = None) -> List[dict]:
+        """Detection stages on host envelopes (drop-in for the env-level functions)."""
+        torch = _torch()
+        fo = np.zeros(len(envs) + 1, dtype=np.int64)
+        fo[1:] = np.cumsum([len(e) for e in envs])   # ds = 1: offsets == decimated offsets
+        d = detect_design(sr, params)
+        out = self.alloc(fo, 1, d.sr)
+        out.env.copy_(torch.from_numpy(np.concatenate(envs).astype(np.float64)).to(self.device))
+        if floors is not None:
+            out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
+        self.run(None, fo, d.sr, params, stages=stages, out=out, d=d)
+        torch.cuda.synchronize(self.device)
+        return out.to_host()
+
+
+def _torch_np_map():
+    torch = _torch()
+    return {np.dtype(np.uint8): torch.uint8, np.dtype(np.int16): torch.int16, np.dtype(np.int32): torch.int32,
+            np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+
+
+_default = {}
+_default_lock = threading.Lock()
+
+
+def default_detector(device: int = 0) -> Detector:
+    with _default_lock:
+        if device not in _default:
+            _default[device] = Detector(device)
+        return _default[device]

@@ -1,0 +1,150 @@
+/*
+ * bpmx.h — C ABI of the MI355X-native heartbeat preprocessing + detection path.
+ *
+ * One shared library (bpm_analysis_amd/libbpmx.so, HIP for gfx950) behind the
+ * reference's own operator surface for this path.  The reference has no
+ * plugin/FFI layer of its own (pure Python); these entry points
+ * replace, one for one, the computation inside:
+ *
+ *   bpmx_run(stages=ENVELOPE)  <- bpm_analysis.py:1007-1062  preprocess_audio
+ *                                 (wavfile.read result -> mean(axis=1) -> [::ds]
+ *                                  -> butter/filtfilt -> |x| rolling mean)
+ *   bpmx_run(stages=FLOOR)     <- bpm_analysis.py:1064-1117  _calculate_dynamic_noise_floor
+ *   bpmx_run(stages=PEAKS)     <- bpm_analysis.py:223-229    PeakClassifier._find_raw_peaks
+ *   bpmx_run(stages=ALL)       <- the three above in sequence, as analyze_wav_file
+ *                                 runs them (bpm_analysis.py:1731-1732, :89)
+ *   bpmx_synth / bpmx_synth_host   deterministic synthetic recordings (bench/tests)
+ *
+ * Plain C types only.  PCM and result arrays are DEVICE pointers (HBM); the
+ * per-file frame offsets are a HOST array.  A batch shares one sample rate,
+ * dtype and channel count; lengths may be ragged.  Filter coefficients
+ * (butter / lfilter_zi / sosfilt_zi) are designed on the host exactly as the
+ * reference designs them and passed in bpmx_params.
+ *
+ * Thread-safety: one bpmx_ctx per thread (or per stream); bpmx_last_error is
+ * thread-local.  Calls may come from a non-main thread (gui.py:181-183).
+ */
+#ifndef BPMX_H
+#define BPMX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BPMX_ABI_VERSION 1
+
+/* sample formats of scipy.io.wavfile.read (bpm_analysis.py:1014) */
+enum bpmx_dtype { BPMX_DT_U8 = 0, BPMX_DT_I16 = 1, BPMX_DT_I32 = 2, BPMX_DT_F32 = 3, BPMX_DT_F64 = 4 };
+
+/* REFERENCE: the shipped pipeline, bit-exact (stride pick, b/a filtfilt at the
+ *            decimated rate, rolling-mean envelope; bpm_analysis.py:1031-1054).
+ * NATIVE:    the north_star ordering (sosfiltfilt at the native rate -> pick
+ *            -> |Hilbert| -> rolling mean); envelope within 1e-9 relative of the
+ *            scipy composition, detection stages identical. */
+enum bpmx_mode { BPMX_MODE_REFERENCE = 0, BPMX_MODE_NATIVE = 1 };
+
+enum bpmx_stage {
+    BPMX_STAGE_ENVELOPE = 1, /* PCM -> env (and y)        */
+    BPMX_STAGE_FLOOR = 2,    /* env -> floor, troughs     */
+    BPMX_STAGE_PEAKS = 4,    /* env, floor -> raw peaks   */
+    BPMX_STAGE_ALL = 7
+};
+
+/* return codes */
+enum bpmx_status {
+    BPMX_OK = 0,
+    BPMX_E_ARG = -1,     /* bad argument (message in bpmx_last_error) */
+    BPMX_E_HIP = -2,     /* HIP runtime error */
+    BPMX_E_LIMIT = -3,   /* a size exceeds what the kernels support */
+    BPMX_E_NODEV = -4    /* no usable gfx950 device */
+};
+
+/* per-file result flags (bpmx_out.flags) */
+enum bpmx_file_flag {
+    BPMX_F_STATIC_FLOOR = 1, /* < 5 troughs: constant quantile floor, troughs unsanitised (:1073-1077) */
+    BPMX_F_DRAFT_FLOOR = 2,  /* <= 2 sanitised troughs: draft floor kept (:1107-1110) */
+    BPMX_F_NAN_FLOOR = 4,    /* all-NaN floor replaced by quantile(env, 0.1) (:1113-1115) */
+    BPMX_F_TOO_SHORT = 8     /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
+};
+
+typedef struct bpmx_ctx bpmx_ctx;
+
+typedef struct {
+    int32_t mode;          /* bpmx_mode */
+    int32_t stages;        /* bpmx_stage mask */
+    int32_t dtype;         /* bpmx_dtype of the PCM */
+    int32_t channels;      /* >= 1, frames are interleaved */
+    int32_t fs;            /* native sample rate */
+    int32_t ds;            /* downsample factor after the clamp (:1021-1029), >= 1 */
+    int32_t sr;            /* decimated rate fs // ds (:1032) */
+    int32_t env_window;    /* sr // 10 (:1053) */
+    int32_t distance;      /* int(min_peak_distance_sec * sr) (:1066, :226), >= 1 */
+    int32_t noise_window;  /* int(noise_window_sec * sr) (:1084) */
+    int32_t min_periods;   /* 3 (:1085, :1105) */
+    int32_t reserved;
+    double trough_prom_q;  /* trough_prominence_quantile (:1067) */
+    double peak_prom_q;    /* peak_prominence_quantile (:225) */
+    double noise_floor_q;  /* noise_floor_quantile (:1075, :1085) */
+    double fallback_q;     /* 0.1 (:1114) */
+    double reject_mult;    /* trough_rejection_multiplier (:1091) */
+    double ba_b[5], ba_a[5], ba_zi[4];  /* butter(2,[lo,hi],'band') at sr + lfilter_zi (reference mode) */
+    double sos[12], sos_zi[4];          /* butter(...,output='sos') at fs + sosfilt_zi (native mode) */
+} bpmx_params;
+
+typedef struct {
+    int32_t n_files;
+    int32_t reserved;
+    const void *pcm;              /* device: frames of all files back to back, interleaved channels */
+    const int64_t *frame_offsets; /* host: n_files+1 frame offsets into pcm */
+} bpmx_batch;
+
+/* Result arrays (device).  Per-file slices start at the decimated offsets
+ * D_f = sum_{g<f} Nd_g, Nd_g = bpmx_decimated_length(frames_g, ds); every
+ * array below has sum(Nd) elements, except the three per-file ones.
+ * env / floor are inputs when the stage that produces them is not requested. */
+typedef struct {
+    double *env;        /* f64 envelope */
+    double *floor;      /* f64 dynamic noise floor */
+    double *y;          /* optional (NULL): filtered decimated signal (debug WAV, :1047-1060) */
+    int64_t *troughs;   /* sanitised trough indices, per-file slice, n_troughs[f] valid */
+    int64_t *peaks;     /* raw peak indices, per-file slice, n_peaks[f] valid */
+    int32_t *n_troughs; /* [n_files] */
+    int32_t *n_peaks;   /* [n_files] */
+    int32_t *flags;     /* [n_files] bpmx_file_flag bits */
+    int32_t *n_raw_troughs; /* optional [n_files]: troughs before sanitisation (:1099 log line) */
+} bpmx_out;
+
+int bpmx_abi_version(void);
+const char *bpmx_last_error(void);
+
+int bpmx_create(int device, bpmx_ctx **out);
+void bpmx_destroy(bpmx_ctx *ctx);
+
+/* ceil(n_frames / ds): length of x[::ds] (:1033) */
+int64_t bpmx_decimated_length(int64_t n_frames, int32_t ds);
+
+/* Run the requested stages over a batch, asynchronously on `stream`
+ * (a hipStream_t; NULL = default stream). */
+int bpmx_run(bpmx_ctx *ctx, const bpmx_params *params, const bpmx_batch *batch, const bpmx_out *out,
+             void *stream);
+
+/* Synthetic int16 recordings straight into HBM: file f gets seed seed0+f,
+ * frames [frame_offsets[f], frame_offsets[f+1]) of pcm (device). */
+int bpmx_synth(bpmx_ctx *ctx, uint64_t seed0, int32_t n_files, const int64_t *frame_offsets, int32_t fs,
+               int32_t channels, int16_t *pcm, void *stream);
+/* The same generator on the host (bit-identical). */
+void bpmx_synth_host(uint64_t seed, int64_t n_frames, int32_t fs, int32_t channels, int16_t *out);
+
+/* Per-kernel device timing with HIP events recorded on the launch stream.
+ * bpmx_profile(ctx, 1) starts recording; bpmx_profile_read() synchronises,
+ * and writes "name launches total_ms\n" lines into buf (returns bytes). */
+int bpmx_profile(bpmx_ctx *ctx, int on);
+int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BPMX_H */

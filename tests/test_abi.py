@@ -1,0 +1,61 @@
+"""C ABI: the library loads, exports every symbol include/bpmx.h declares, and
+its host-only entry points behave (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from bpm_analysis_amd import _native as N
+from oracle import oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    txt = open(os.path.join(REPO, "include", "bpmx.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|int64_t|const char \*)\s*\**\s*(bpmx_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_matches_binding_list():
+    assert _declared() == sorted(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.load()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert L.bpmx_abi_version() == N.ABI_VERSION
+
+
+def test_struct_layouts():
+    # offsets the C side relies on (bpmx_params: 12 int32, then doubles)
+    assert N.Params.trough_prom_q.offset == 48
+    assert N.Params.ba_b.offset == 48 + 5 * 8
+    assert ctypes.sizeof(N.Params) == 48 + 5 * 8 + (5 + 5 + 4 + 12 + 4) * 8
+    assert ctypes.sizeof(N.Batch) == 24
+    assert ctypes.sizeof(N.Out) == 9 * 8
+
+
+@pytest.mark.parametrize("n,ds,want", [(2646000, 146, 18124), (146 * 15, 146, 15), (1, 300, 1), (0, 5, 0)])
+def test_decimated_length(n, ds, want):
+    assert N.load().bpmx_decimated_length(n, ds) == want
+
+
+@pytest.mark.parametrize("seed,fs,ch", [(0, 44100, 1), (3, 96000, 2), (9, 22050, 1)])
+def test_synth_host_matches_oracle_generator(seed, fs, ch):
+    n = fs * 2 + 17
+    out = np.empty(n * ch, dtype=np.int16)
+    N.load().bpmx_synth_host(seed, n, fs, ch, out.ctypes.data)
+    assert np.array_equal(out, O.synth(seed, n, fs, ch).reshape(-1))
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    c = ctypes.c_void_p()
+    rc = N.load().bpmx_create(0, ctypes.byref(c))
+    assert rc == N.E_NODEV
+    assert b"device" in N.load().bpmx_last_error()
