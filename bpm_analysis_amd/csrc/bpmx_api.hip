@@ -268,7 +268,19 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             std::memcpy(a.a, P->ba_a, sizeof a.a);
             std::memcpy(a.zi, P->ba_zi, sizeof a.zi);
             a.scratch = scr; a.env = O->env; a.y = O->y;
-            LAUNCH(ctx, s, "k_envelope_ref", k_envelope_ref, dim3((F + 63) / 64), dim3(64), 0, s, a);
+            const bool multi = P->channels > 1;
+            const dim3 g((F + 63) / 64), b(64);
+#define ENV_REF(DT)                                                                                  \
+    if (multi) LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, true>), g, b, 0, s, a);         \
+    else LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, false>), g, b, 0, s, a);
+            switch (P->dtype) {
+            case BPMX_DT_U8: ENV_REF(BPMX_DT_U8) break;
+            case BPMX_DT_I16: ENV_REF(BPMX_DT_I16) break;
+            case BPMX_DT_I32: ENV_REF(BPMX_DT_I32) break;
+            case BPMX_DT_F32: ENV_REF(BPMX_DT_F32) break;
+            default: ENV_REF(BPMX_DT_F64) break;
+            }
+#undef ENV_REF
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
             if (r != BPMX_OK) return r;
@@ -293,10 +305,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         QuantArgs a;
         a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv;
         int L = 0;
-        auto add = [&](double q, int slot) {
+        auto add = [&](double q, int slot) {      /* one radix select per distinct level */
             for (int l = 0; l < L; ++l)
-                if (a.q[l] == q && a.slot[l] == slot) return;
-            a.q[L] = q; a.slot[L] = slot; ++L;
+                if (a.q[l] == q) { a.slot[l] |= 1 << slot; return; }
+            a.q[L] = q; a.slot[L] = 1 << slot; ++L;
         };
         if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->noise_floor_q, Q_NOISE); add(P->fallback_q, Q_FALLBACK); }
         if (do_peaks) add(P->peak_prom_q, Q_PEAK);
@@ -320,30 +332,24 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
         const int64_t W = P->noise_window;
-        int T = 256;
-        int cap = (int)((W + T + 64 + 63) / 64 * 64);
-        size_t lds = rollq_lds_bytes(T, cap);
-        if (lds > 80 * 1024) {
-            T = 128;
-            cap = (int)((W + T + 64 + 63) / 64 * 64);
-            lds = rollq_lds_bytes(T, cap);
-        }
-        if (lds > 160 * 1024 || W + T >= 65000)
+        const int cap = (int)((W + RQ_T - 1 + 63) / 64 * 64);
+        const size_t lds = rollq_lds_bytes(RQ_T, cap);
+        if (cap > 32 * RQ_T || W + RQ_T >= 65000)
             return fail(BPMX_E_LIMIT, "noise window of " + std::to_string(W) +
-                                          " samples exceeds the LDS rolling-quantile kernel (max ~6000)");
+                                          " samples exceeds the rolling-quantile kernel (max 7800)");
         auto rollq = [&](const int32_t *run, const int64_t *tr, double *outp, int32_t *allnan) -> int {
             RollqArgs a;
             a.dense = dense; a.doff = d_doff; a.troughs = tr; a.run = run; a.n_files = F;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
             a.out = outp; a.allnan = allnan;
-            if (T == 256) {
-                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<256>,
+            if (cap <= 16 * RQ_T) {
+                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 16>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_rolling_quantile", k_rolling_quantile<256>, dim3(F), dim3(256), lds, s, a);
+                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 16>), dim3(F), dim3(RQ_T), lds, s, a);
             } else {
-                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<128>,
+                (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 32>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_rolling_quantile", k_rolling_quantile<128>, dim3(F), dim3(128), lds, s, a);
+                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 32>), dim3(F), dim3(RQ_T), lds, s, a);
             }
             return BPMX_OK;
         };

@@ -28,7 +28,7 @@ struct QuantArgs {
     const int64_t *doff;
     const int32_t *active;
     int32_t n_files, n_levels;
-    int32_t slot[Q_SLOTS];  /* qv slot written by level l */
+    int32_t slot[Q_SLOTS];  /* bitmask of the qv slots level l fills */
     double q[Q_SLOTS];
     double *qv;             /* [F][Q_SLOTS] */
 };
@@ -80,6 +80,9 @@ struct RollqArgs {
     double q;
     double *out;
     int32_t *allnan;         /* [F] */
+#ifdef BPMX_STAMPS
+    unsigned long long *stamps;
+#endif
 };
 
 struct SanitizeArgs {
@@ -107,22 +110,25 @@ struct FinalArgs {
     int32_t *flags;
 };
 
-/* dynamic LDS bytes of k_rolling_quantile<T> for a union capacity `cap`
- * (multiple of 64): Av,Bv f64[cap]; nv,nsv f64[T]; ebits u64[cap/64+2];
- * Ap,Bp u16[cap]; rem u16[cap+4]; nsp u16[T+4]; scan scratch int[64]. */
+/* dynamic LDS bytes of k_rolling_quantile<T,...> for a union capacity `cap`
+ * (multiple of 64, >= W+T-1): Av f64[cap]; nsv f64[T]; runv f64[T] (later the
+ * edge list); Ap u16[cap]; nsp,ubv u16[T]; rpref int[T+1] (later the edge-word
+ * prefix, needs cap/64+2 <= T+1); scan scratch int[T/64+2].
+ * 39.4 KB at W=3020, T=256: four workgroups per CU. */
 __host__ __device__ inline size_t rollq_lds_bytes(int T, int cap) {
-    return (size_t)cap * 16 + (size_t)T * 16 + ((size_t)cap / 64 + 2) * 8 + (size_t)cap * 4 + ((size_t)cap + 4) * 2 +
-           ((size_t)T + 4) * 2 + 64 * 4;
+    return (size_t)cap * 10 + (size_t)T * 20 + ((size_t)T + 1) * 4 + ((size_t)T / 64 + 2) * 4;
 }
+constexpr int RQ_T = 256;   /* outputs per tile = threads per workgroup */
 
-__global__ void k_envelope_ref(EnvRefArgs A);
+template <int DT, bool MULTI>
+__global__ void k_envelope_ref_t(EnvRefArgs A);
 __global__ void k_quantile(QuantArgs A);
 __global__ void k_block_stats(BlockStatArgs A);
 __global__ void k_find_peaks(PeakArgs A);
 __global__ void k_interp(InterpArgs A);
 __global__ void k_sanitize(SanitizeArgs A);
 __global__ void k_floor_final(FinalArgs A);
-template <int T>
+template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);
 
 }  // namespace bpmx

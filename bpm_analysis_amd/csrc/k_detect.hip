@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
         const double vb = (c > lo + 1) ? va : key_f64(m);
         res = np_lerp(va, vb, vi - (double)lo);
     }
-    if (tid == 0) A.qv[(int64_t)f * Q_SLOTS + A.slot[l]] = res;
+    if (tid < Q_SLOTS && ((A.slot[l] >> tid) & 1)) A.qv[(int64_t)f * Q_SLOTS + tid] = res;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -7,20 +7,49 @@
  *   dtype, DF-II-transposed recursion of _sigtools._linear_filter) -> |y| ->
  *   pandas centred rolling mean, Kahan add/remove (:1052-1054).
  *
- * Bit-exactness forces a strictly sequential recursion per file, so the
- * parallelism is across files: one lane per recording.  The forward-pass
- * output is parked in an interleaved scratch [step][file] so the 64 lanes of
- * a wave touch one contiguous 512-B row per step (coalesced), the backward
- * pass overwrites it in place with y, and the rolling mean streams it again.
- * The strided PCM gather (one int16 every ds frames) is software-pipelined
- * eight samples ahead so HBM latency overlaps the f64 recursion.
- * Roofline: neither HBM nor VALU — it is the latency of ~3 dependent f64
- * ops per step times 2*(Nd+30) + Nd steps.
+ * Bit-exactness forces a strictly sequential recursion per recording, so the
+ * parallelism is across recordings: one lane per file, 64 files per wave.
+ * What remains is a latency problem, and the kernel is built around it:
+ *  - the forward output is parked in an interleaved scratch [step][file] so
+ *    the 64 lanes of a wave touch one contiguous 512-B row per step;
+ *  - every sequential stream (the stride-ds PCM gather, the scratch read of
+ *    the backward pass, the add and remove streams of the rolling mean) is
+ *    software-pipelined one 16-step block ahead in registers, so a block's
+ *    loads are in flight while the previous block's f64 recursion runs;
+ *  - env / y rows are transposed through LDS and written 512 B per
+ *    instruction instead of 64 scattered 8-B stores.
+ * Roofline: the f64 dependency chain (~3 dependent ops per step, ~17 ops
+ * issued per step by one wave) — neither HBM nor VALU throughput.
  */
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 
 namespace bpmx {
+
+/* ---- compile-time PCM loaders (frame value after the channel mean) ---- */
+template <int DT>
+struct Pcm;
+template <> struct Pcm<BPMX_DT_U8> { typedef uint8_t T; };
+template <> struct Pcm<BPMX_DT_I16> { typedef int16_t T; };
+template <> struct Pcm<BPMX_DT_I32> { typedef int32_t T; };
+template <> struct Pcm<BPMX_DT_F32> { typedef float T; };
+template <> struct Pcm<BPMX_DT_F64> { typedef double T; };
+
+template <int DT, bool MULTI>
+__device__ __forceinline__ double frame_at(const void *__restrict__ pcm, int ch, int64_t frame) {
+    typedef typename Pcm<DT>::T T;
+    const T *p = (const T *)pcm;
+    if (!MULTI) return (double)p[frame];
+    if (DT == BPMX_DT_F32) {
+        const float *q = (const float *)pcm + frame * ch;
+        float s = q[0];
+        for (int c = 1; c < ch; ++c) s = s + q[c];
+        return (double)(s / (float)ch);
+    }
+    double s = (double)p[frame * ch];
+    for (int c = 1; c < ch; ++c) s = s + (double)p[frame * ch + c];
+    return s / (double)ch;
+}
 
 struct Df2t {
     double b0, b1, b2, b3, b4, a1, a2, a3, a4;
@@ -34,9 +63,12 @@ struct Df2t {
         z3 = xn * b4 - yn * a4;
         return yn;
     }
+    __device__ __forceinline__ void init(const double *zi, double x0) {
+        z0 = zi[0] * x0; z1 = zi[1] * x0; z2 = zi[2] * x0; z3 = zi[3] * x0;
+    }
 };
 
-/* pandas roll_mean state (aggregations.pyx add_mean/remove_mean/calc_mean) */
+/* pandas roll_mean state (aggregations.pyx add_mean / remove_mean / calc_mean) */
 struct RollMean {
     double sum = 0, cadd = 0, crem = 0, prev = 0;
     int64_t nobs = 0, neg = 0, same = 0;
@@ -60,8 +92,8 @@ struct RollMean {
             if (__signbit(v)) neg--;
         }
     }
-    __device__ __forceinline__ double mean(int64_t minp) const {
-        if (nobs >= minp && nobs > 0) {
+    __device__ __forceinline__ double mean() const {
+        if (nobs >= 1) {
             double r = sum / (double)nobs;
             if (same >= nobs) r = prev;
             else if (neg == 0 && r < 0) r = 0;
@@ -72,100 +104,184 @@ struct RollMean {
     }
 };
 
-/* Kahan rolling mean of |v| where v(j) = src[j*S] (interleaved scratch).
- * Writes env[i] (and y[i] = v(i) when y != nullptr). */
-__device__ __forceinline__ void rolling_mean_abs(const double *src, int64_t S, int64_t n, int64_t w,
-                                                 double *env, double *y) {
-    RollMean R;
-    int64_t ps = 0, pe = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        int64_t s, e;
-        win_bounds(i, n, w, s, e);
-        if (i == 0 || s >= pe) {
-            R = RollMean();
-            R.prev = fabs(src[s * S]);
-            for (int64_t j = s; j < e; ++j) R.add(fabs(src[j * S]));
-        } else {
-            for (int64_t j = ps; j < s; ++j) R.remove(fabs(src[j * S]));
-            for (int64_t j = pe; j < e; ++j) R.add(fabs(src[j * S]));
-        }
-        env[i] = R.mean(1);
-        if (y) y[i] = src[i * S];
-        ps = s;
-        pe = e;
+constexpr int PF = 16;   /* prefetch block (steps) */
+constexpr int STG = 64;  /* LDS staging rows */
+
+/* write the staged rows [base, base+rows) of every file in the wave, 512 B per store */
+__device__ __forceinline__ void flush_rows(double (*stage)[65], double *__restrict__ dst, int64_t base, int rows,
+                                           int64_t my_d0, int64_t my_nd) {
+    const int lane = lane_id();
+    for (int fl = 0; fl < 64; ++fl) {
+        const int64_t d0 = __shfl(my_d0, fl);
+        const int64_t nd = __shfl(my_nd, fl);
+        const int64_t i = base + lane;
+        if (lane < rows && i < nd) dst[d0 + i] = stage[lane][fl];
     }
 }
 
-__global__ __launch_bounds__(64) void k_envelope_ref(EnvRefArgs A) {
-    const int f = blockIdx.x * 64 + threadIdx.x;
-    if (f >= A.n_files) return;
-    const int64_t nd = A.doff[f + 1] - A.doff[f];
-    if (nd <= 15 || !A.active[f]) return;
-    const int64_t fb = A.foff[f];
-    const int wdt = work_dtype(A.dtype, A.channels);
-    const int64_t S = A.n_files;
-    const int64_t ne = nd + 30;
+template <int DT, bool MULTI>
+__global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
+    __shared__ double st_env[STG][65];
+    __shared__ double st_y[STG][65];
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x * 64 + lane;
+    const bool have = f < A.n_files;
+    int64_t nd = have ? A.doff[f + 1] - A.doff[f] : 0;
+    const bool run = have && nd > 15 && A.active[f];
+    if (!run) nd = 0;
+    const int64_t d0 = have ? A.doff[f] : 0;
+    const int64_t fb = have ? A.foff[f] : 0;
     const int64_t ds = A.ds;
-    double *scr = A.scratch + f;
+    const int ch = A.channels;
+    const int wdt = work_dtype(DT, MULTI ? 2 : 1);
+    const int64_t S = A.n_files;
+    const void *__restrict__ pcm = A.pcm;
+    double *__restrict__ scr = A.scratch + (have ? f : 0);
+    /* wave-uniform trip counts (ragged files: lanes past their end are masked) */
+    int64_t ndmax = nd;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmax, o); ndmax = t > ndmax ? t : ndmax; }
+    if (ndmax == 0) return;
 
     Df2t D;
     D.b0 = A.b[0]; D.b1 = A.b[1]; D.b2 = A.b[2]; D.b3 = A.b[3]; D.b4 = A.b[4];
     D.a1 = A.a[1]; D.a2 = A.a[2]; D.a3 = A.a[3]; D.a4 = A.a[4];
+    const int64_t last = nd > 0 ? nd - 1 : 0;
+    auto xd = [&](int64_t j) -> double {
+        j = j < 0 ? 0 : (j > last ? last : j);
+        return frame_at<DT, MULTI>(pcm, ch, fb + j * ds);
+    };
 
-    const double x0 = frame_value(A.pcm, A.dtype, A.channels, fb);
-    const double xl = frame_value(A.pcm, A.dtype, A.channels, fb + (nd - 1) * ds);
-    /* forward pass, left pad: ext[j] = 2*x0 - xd[15-j] in the input dtype */
-    double e0 = odd_ext(wdt, x0, frame_value(A.pcm, A.dtype, A.channels, fb + 15 * ds));
-    D.z0 = A.zi[0] * e0; D.z1 = A.zi[1] * e0; D.z2 = A.zi[2] * e0; D.z3 = A.zi[3] * e0;
-    for (int j = 0; j < 15; ++j) {
-        double xn = odd_ext(wdt, x0, frame_value(A.pcm, A.dtype, A.channels, fb + (15 - j) * ds));
-        scr[j * S] = D.step(xn);
-    }
-    /* body: xd[j], gathered 8 ahead */
+    /* ---------------- forward pass ---------------- */
     {
-        double cur[8], nxt[8];
+        double padv[15], padr[15];
+        const double x0 = xd(0), xl = xd(last);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            int64_t jj = u < nd ? u : nd - 1;
-            cur[u] = frame_value(A.pcm, A.dtype, A.channels, fb + jj * ds);
+        for (int k = 0; k < 15; ++k) { padv[k] = xd(15 - k); padr[k] = xd(last - 1 - k); }
+        double cur[PF], nxt[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) cur[u] = xd(u);
+        if (run) {
+            const double e0 = odd_ext(wdt, x0, padv[0]);
+            D.init(A.zi, e0);
+#pragma unroll
+            for (int k = 0; k < 15; ++k) scr[k * S] = D.step(odd_ext(wdt, x0, padv[k]));
         }
-        for (int64_t j = 0; j < nd; j += 8) {
+        for (int64_t j0 = 0; j0 < ndmax; j0 += PF) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                int64_t jj = j + 8 + u;
-                jj = jj < nd ? jj : nd - 1;
-                nxt[u] = frame_value(A.pcm, A.dtype, A.channels, fb + jj * ds);
+            for (int u = 0; u < PF; ++u) nxt[u] = xd(j0 + PF + u);
+            if (run) {
+#pragma unroll
+                for (int u = 0; u < PF; ++u)
+                    if (j0 + u < nd) scr[(15 + j0 + u) * S] = D.step(cur[u]);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (j + u < nd) scr[(15 + j + u) * S] = D.step(cur[u]);
+            for (int u = 0; u < PF; ++u) cur[u] = nxt[u];
+        }
+        if (run) {
+#pragma unroll
+            for (int k = 0; k < 15; ++k) scr[(15 + nd + k) * S] = D.step(odd_ext(wdt, xl, padr[k]));
+        }
+    }
+    /* ---------------- backward pass, in place ---------------- */
+    {
+        const int64_t ne = nd + 30;
+        const int64_t nemax = ndmax + 30;
+        /* lane-local reversed index r -> scratch row ne-1-r; lanes with r >= ne idle */
+        auto ld = [&](int64_t r) -> double {
+            int64_t row = ne - 1 - r;
+            row = row < 0 ? 0 : row;
+            return scr[row * S];
+        };
+        double cur[PF], nxt[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) cur[u] = ld(u);
+        if (run) D.init(A.zi, cur[0]);
+        for (int64_t r0 = 0; r0 < nemax; r0 += PF) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) nxt[u] = ld(r0 + PF + u);
+            if (run) {
+#pragma unroll
+                for (int u = 0; u < PF; ++u)
+                    if (r0 + u < ne) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+            for (int u = 0; u < PF; ++u) cur[u] = nxt[u];
         }
     }
-    /* right pad: ext[15+nd+k] = 2*xl - xd[nd-2-k] */
-    for (int k = 0; k < 15; ++k) {
-        double xn = odd_ext(wdt, xl, frame_value(A.pcm, A.dtype, A.channels, fb + (nd - 2 - k) * ds));
-        scr[(15 + nd + k) * S] = D.step(xn);
-    }
-    /* backward pass over the reversed forward output, in place */
+    /* ---------------- |y| centred rolling mean over rows [15, 15+nd) ---------------- */
     {
-        const double y0 = scr[(ne - 1) * S];
-        D.z0 = A.zi[0] * y0; D.z1 = A.zi[1] * y0; D.z2 = A.zi[2] * y0; D.z3 = A.zi[3] * y0;
-        int64_t j = ne - 1;
-        for (; j >= 7; j -= 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = scr[(j - u) * S];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) scr[(j - u) * S] = D.step(v[u]);
+        const double *__restrict__ y = scr + 15 * S;
+        const int64_t w = A.env_window;
+        const int64_t off = (w - 1) / 2;
+        double *__restrict__ env = A.env;
+        double *__restrict__ yout = A.y;
+        auto ldy = [&](int64_t i) -> double {
+            i = i < 0 ? 0 : (i > last ? last : i);
+            return fabs(y[i * S]);
+        };
+        RollMean R;
+        /* i = 0: setup window [0, e0) */
+        const int64_t e0 = (1 + off) < nd ? (1 + off) : nd;
+        if (run) {
+            R.prev = ldy(0);
+            for (int64_t j = 0; j < e0; ++j) R.add(ldy(j));
         }
-        for (; j >= 0; --j) scr[j * S] = D.step(scr[j * S]);
+        double ca[PF], cr[PF], na[PF], nr[PF], cy[PF], ny[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            ca[u] = ldy(u + off); cr[u] = ldy(u + off - w);
+            cy[u] = yout ? y[(u < last ? u : last) * S] : 0.0;
+        }
+        for (int64_t i0 = 0; i0 < ndmax; i0 += PF) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int64_t i = i0 + PF + u;
+                na[u] = ldy(i + off);
+                nr[u] = ldy(i + off - w);
+                if (yout) ny[u] = y[(i < last ? i : last) * S];
+            }
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int64_t i = i0 + u;
+                double ev = 0.0;
+                if (run && i < nd) {
+                    if (w == 1) {
+                        R = RollMean();
+                        R.prev = ca[u];
+                        R.add(ca[u]);
+                    } else if (i > 0) {
+                        const int64_t s = i + 1 + off - w;      /* unclipped start; remove when it advances */
+                        if (s > 0 && s <= nd) R.remove(cr[u]);
+                        if (i + off < nd) R.add(ca[u]);
+                    }
+                    ev = R.mean();
+                }
+                st_env[(i0 + u) & (STG - 1)][lane] = ev;
+                if (yout) st_y[(i0 + u) & (STG - 1)][lane] = cy[u];
+            }
+            if (((i0 + PF) & (STG - 1)) == 0 || i0 + PF >= ndmax) {
+                const int64_t base = (i0 + PF - 1) & ~(int64_t)(STG - 1);
+                const int rows = (int)(i0 + PF - base);
+                __syncthreads();
+                flush_rows(st_env, env, base, rows, d0, nd);
+                if (yout) flush_rows(st_y, yout, base, rows, d0, nd);
+                __syncthreads();
+            }
+#pragma unroll
+            for (int u = 0; u < PF; ++u) { ca[u] = na[u]; cr[u] = nr[u]; cy[u] = ny[u]; }
+        }
     }
-    /* |y| centred rolling mean over the trimmed range [15, 15+nd) */
-    const int64_t d0 = A.doff[f];
-    rolling_mean_abs(scr + 15 * S, S, nd, A.env_window, A.env + d0, A.y ? A.y + d0 : nullptr);
 }
+
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F32, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F64, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F32, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F64, true>(EnvRefArgs);
 
 }  // namespace bpmx

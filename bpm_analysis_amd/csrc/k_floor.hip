@@ -27,6 +27,29 @@
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 
+/* Optional in-kernel phase timing (tools/kbench.hip builds with -DBPMX_STAMPS;
+ * the library never does): thread 0 accumulates s_memtime deltas per phase. */
+#ifdef BPMX_STAMPS
+#define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(k)                                                                  \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            unsigned long long _t = __builtin_amdgcn_s_memtime();                 \
+            _st_acc[k] += _t - _st_t;                                             \
+            _st_t = _t;                                                           \
+        }                                                                         \
+    } while (0)
+#define STAMP_FLUSH(ptr)                                                          \
+    do {                                                                          \
+        if (threadIdx.x == 0 && (ptr))                                            \
+            for (int _k = 0; _k < 8; ++_k) (ptr)[blockIdx.x * 8 + _k] = _st_acc[_k]; \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k) do {} while (0)
+#define STAMP_FLUSH(ptr) do {} while (0)
+#endif
+
 namespace bpmx {
 
 __global__ __launch_bounds__(256) void k_interp(InterpArgs A) {
@@ -76,35 +99,42 @@ __device__ __forceinline__ int upper_bound_lds(const double *a, int n, double v)
     return lo;
 }
 
-template <int T>
+template <int T, int RQ_MAXCH>
 __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
     extern __shared__ __align__(16) unsigned char smem[];
     const int cap = A.cap;
-    double *Av = (double *)smem;
-    double *Bv = Av + cap;
-    double *nv = Bv + cap;          /* [T] new values in position order */
-    double *nsv = nv + T;           /* [T] new values sorted */
-    unsigned long long *ebits = (unsigned long long *)(nsv + T);   /* [cap/64+2] */
-    uint16_t *Ap = (uint16_t *)(ebits + cap / 64 + 2);
-    uint16_t *Bp = Ap + cap;
-    uint16_t *rem = Bp + cap;       /* [cap+1] exclusive prefix of removed flags */
-    uint16_t *nsp = rem + cap + 4;  /* [T] positions of sorted new values */
-    int *sh = (int *)(nsp + T + 4); /* scan scratch */
-    __shared__ int s_first, s_last;
+    /* LDS carve-up (rollq_lds_bytes); single sorted buffer A: a merge reads the
+     * thread's slice of A into registers, barriers, then writes the merged order. */
+    double *Av = (double *)smem;                     /* [cap] sorted union values */
+    double *nsv = Av + cap;                          /* [T] new values, sorted */
+    double *runv = nsv + T;                          /* [T] per-wave sorted runs | edge list */
+    uint32_t *E = (uint32_t *)runv;                  /*     (aliases runv after the merge) */
+    uint16_t *Ap = (uint16_t *)(runv + T);           /* [cap] positions mod 2^16 */
+    uint16_t *nsp = Ap + cap;                        /* [T] */
+    uint16_t *ubv = nsp + T;                         /* [T] */
+    int *rpref = (int *)(ubv + T);                   /* [T+1] removed prefix | edge-word prefix */
+    int *wpre = rpref;                               /*     (cap/64+2 <= T+1 entries, edge phase) */
+    int *sh = rpref + T + 1;                         /* [T/64+2] */
+    __shared__ int s_first, s_last, s_nE;
 
-    const int tid = threadIdx.x, lane = lane_id();
+    const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const double *dense = A.dense + d0;
     double *out = A.out + d0;
     const int64_t W = A.window, minp = A.min_periods;
     const int64_t t0 = A.troughs[d0];
     const double q = A.q;
+    const double INF = __builtin_inf();
     if (tid == 0) { s_first = INT_MAX; s_last = -1; }
+    STAMP_DECL
 
     int nA = 0;
     int64_t P0prev = 0, P1prev = 0;
+    /* the next tile's first chunk of new samples is loaded during this tile's walk */
+    double vpre = INF;
+    int64_t apre = -1;
     for (int64_t i0 = 0; i0 < n; i0 += T) {
         const int64_t i1 = i0 + T < n ? i0 + T : n;
         int64_t sA, eA, sB, eB;
@@ -112,154 +142,230 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
         win_bounds(i1 - 1, n, W, sB, eB);
         const int64_t P0 = sA > t0 ? sA : t0;
         const int64_t P1 = eB > P0 ? eB : P0;
-        /* ---- removal of positions < P0 ---- */
+        STAMP(7);
+        /* ---- positions < P0 leave, [max(P1prev,P0), P1) enter (chunks of <= T) ---- */
         bool pending_rem = false;
         if (nA > 0 && P0 > P0prev) {
-            if (P0 >= P1prev) {
-                nA = 0;
-            } else {
-                pending_rem = true;
-                const int cut = (int)(P0 - P0prev);
-                const uint16_t b16 = (uint16_t)P0prev;
-                const int ch = (nA + T - 1) / T;
-                const int j0 = tid * ch, j1 = j0 + ch < nA ? j0 + ch : nA;
-                int cnt = 0;
-                for (int j = j0; j < j1; ++j) cnt += ((uint16_t)(Ap[j] - b16) < cut) ? 1 : 0;
-                int tot;
-                int pre = block_scan_int<T>(cnt, sh, &tot);
-                for (int j = j0; j < j1; ++j) {
-                    rem[j] = (uint16_t)pre;
-                    pre += ((uint16_t)(Ap[j] - b16) < cut) ? 1 : 0;
-                }
-                if (tid == 0) rem[nA] = (uint16_t)tot;
-                __syncthreads();
-            }
+            if (P0 >= P1prev) nA = 0;
+            else pending_rem = true;
         }
-        /* ---- insert new positions [max(P1prev,P0), P1) in chunks of T ---- */
-        int64_t a = P1prev > P0 ? P1prev : P0;
         const uint16_t b16 = (uint16_t)P0prev;
         const int cut = (int)(P0 - P0prev);
+        int64_t a = P1prev > P0 ? P1prev : P0;
         do {
             const int64_t b = a + T < P1 ? a + T : P1;
             const int nn = b > a ? (int)(b - a) : 0;
             if (nn == 0 && !pending_rem) break;
-            double v = 0;
-            if (tid < nn) { v = dense[a + tid]; nv[tid] = v; }
-            __syncthreads();
-            if (tid < nn) {
-                int r = 0;
-                for (int u = 0; u < nn; ++u) {
-                    const double w = nv[u];
-                    r += (w < v || (w == v && u < tid)) ? 1 : 0;
+            /* (1) this thread's slice of A into registers, removed flags counted */
+            const int CH = (nA + T - 1) / T;
+            const int j0 = tid * CH < nA ? tid * CH : nA;
+            const int j1 = j0 + CH < nA ? j0 + CH : nA;
+            double ov[RQ_MAXCH];
+            uint16_t op[RQ_MAXCH];
+            int rc = 0;
+#pragma unroll
+            for (int c = 0; c < RQ_MAXCH; ++c) {
+                if (j0 + c < j1) {
+                    ov[c] = Av[j0 + c];
+                    op[c] = Ap[j0 + c];
+                    rc += (pending_rem && (uint16_t)(op[c] - b16) < cut) ? 1 : 0;
                 }
+            }
+            /* (2) sort the new values: bitonic per wave in registers, then rank across runs */
+            double v = (a == apre) ? vpre : (tid < nn ? dense[a + tid] : INF);
+            int p = tid;
+            for (int k = 2; k <= 64; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const double vo = __shfl_xor(v, j);
+                    const int po = __shfl_xor(p, j);
+                    const bool other_less = vo < v || (vo == v && po < p);
+                    const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+                    if (lower == up ? other_less : !other_less) { v = vo; p = po; }
+                }
+            }
+            runv[tid] = v;
+            int rtot;
+            const int rpre = block_scan_int<T>(rc, sh, &rtot);   /* barriers: runs visible after */
+            STAMP(0);
+            rpref[tid] = rpre;
+            if (tid == 0) rpref[T] = rtot;
+            int ub = 0, r = lane;
+            if (p < nn) {
+                for (int w2 = 0; w2 < T / 64; ++w2) {
+                    if (w2 == wid) continue;
+                    const double *rv = runv + w2 * 64;
+                    int lo3 = 0, hi3 = 64;
+                    if (w2 < wid) {   /* earlier positions: equal values rank before */
+                        while (lo3 < hi3) { int mid = (lo3 + hi3) >> 1; if (rv[mid] <= v) lo3 = mid + 1; else hi3 = mid; }
+                    } else {
+                        while (lo3 < hi3) { int mid = (lo3 + hi3) >> 1; if (rv[mid] < v) lo3 = mid + 1; else hi3 = mid; }
+                    }
+                    r += lo3;
+                }
+                /* insertion point among the old values (ties: new after old) */
+                ub = upper_bound_lds(Av, nA, v);
                 nsv[r] = v;
-                nsp[r] = (uint16_t)(a + tid);
+                nsp[r] = (uint16_t)(a + p);
+                ubv[r] = (uint16_t)ub;
             }
             __syncthreads();
-            int kept = nA;
-            if (pending_rem) kept = nA - rem[nA];
-            for (int j = tid; j < nA; j += T) {
-                int kb = j;
-                if (pending_rem) {
-                    if ((uint16_t)(Ap[j] - b16) < cut) continue;
-                    kb = j - rem[j];
+            STAMP(1);
+            /* (3) destinations: old j -> j - removed_before(j) + #{new with ub <= j};
+             *                   new rank r -> r + ub - removed_before(ub) */
+            int odst[RQ_MAXCH];
+            {
+                int lo2 = 0, hi2 = nn;
+                while (lo2 < hi2) { int mid = (lo2 + hi2) >> 1; if (ubv[mid] <= j0) lo2 = mid + 1; else hi2 = mid; }
+                int ptr = lo2, rm = rpre;
+#pragma unroll
+                for (int c = 0; c < RQ_MAXCH; ++c) {
+                    odst[c] = -1;
+                    if (j0 + c < j1) {
+                        const int j = j0 + c;
+                        while (ptr < nn && ubv[ptr] <= j) ptr++;
+                        if (pending_rem && (uint16_t)(op[c] - b16) < cut) { rm++; continue; }
+                        odst[c] = j - rm + ptr;
+                    }
                 }
-                const double ov = Av[j];
-                const int dst = kb + lower_bound_lds(nsv, nn, ov);
-                Bv[dst] = ov;
-                Bp[dst] = Ap[j];
             }
-            if (tid < nn) {
-                const double w = nsv[tid];
-                const int ub = upper_bound_lds(Av, nA, w);
-                const int kb = pending_rem ? ub - rem[ub] : ub;
-                Bv[tid + kb] = w;
-                Bp[tid + kb] = nsp[tid];
+            int ndst = -1;
+            if (p < nn) {
+                int rb = 0;
+                if (pending_rem) {
+                    const int c = CH > 0 ? (ub / CH < T ? ub / CH : T) : 0;
+                    rb = rpref[c];
+                    for (int j = c * CH; j < ub; ++j) rb += ((uint16_t)(Ap[j] - b16) < cut) ? 1 : 0;
+                }
+                ndst = r + ub - rb;
             }
             __syncthreads();
-            { double *tv = Av; Av = Bv; Bv = tv; uint16_t *tp = Ap; Ap = Bp; Bp = tp; }
-            nA = kept + nn;
+            /* (4) write the merged order in place */
+#pragma unroll
+            for (int c = 0; c < RQ_MAXCH; ++c)
+                if (j0 + c < j1 && odst[c] >= 0) { Av[odst[c]] = ov[c]; Ap[odst[c]] = op[c]; }
+            if (ndst >= 0) { Av[ndst] = v; Ap[ndst] = (uint16_t)(a + p); }
+            __syncthreads();
+            STAMP(2);
+            nA = nA - rtot + nn;
             pending_rem = false;
             a = b;
         } while (a < P1);
         P0prev = P0;
         P1prev = P1 > P1prev ? P1 : P1prev;
+        if (i0 + T < n) {   /* prefetch the next tile's first chunk of new samples */
+            const int64_t i0n = i0 + T, i1n = i0n + T < n ? i0n + T : n;
+            int64_t sAn, eAn, sBn, eBn;
+            win_bounds(i0n, n, W, sAn, eAn);
+            win_bounds(i1n - 1, n, W, sBn, eBn);
+            const int64_t P0n = sAn > t0 ? sAn : t0;
+            const int64_t P1n = eBn > P0n ? eBn : P0n;
+            const int64_t an = P1prev > P0n ? P1prev : P0n;
+            const int64_t bn = an + T < P1n ? an + T : P1n;
+            apre = an;
+            vpre = (an + tid < bn) ? dense[an + tid] : INF;
+        }
 
-        /* ---- edge bitmap over the sorted union ---- */
-        const int64_t LE = sB > t0 ? sB : t0;   /* left edge: positions < LE may be excluded */
-        const int64_t RE = eA;                   /* right edge: positions >= RE may be excluded */
+        /* ---- edge list: sorted indices whose position may be outside some window of the tile ---- */
+        const int64_t LE = sB > t0 ? sB : t0;   /* positions < LE: left edge */
+        const int64_t RE = eA;                   /* positions >= RE: right edge */
         const int relLE = (int)(LE - P0), relRE = (int)(RE - P0);
         const uint16_t p16 = (uint16_t)P0;
         const int nwords = (nA + 63) >> 6;
-        for (int w = wave_id(); w < nwords; w += T / 64) {
+        for (int w = wid; w < nwords; w += T / 64) {
             const int j = (w << 6) + lane;
-            bool bit = false;
-            if (j < nA) {
-                const int rel = (uint16_t)(Ap[j] - p16);
-                bit = rel < relLE || rel >= relRE;
-            }
+            const int rel = j < nA ? (int)(uint16_t)(Ap[j] - p16) : 0;
+            const bool bit = j < nA && (rel < relLE || rel >= relRE);
             const unsigned long long word = __ballot(bit);
-            if (lane == 0) ebits[w] = word;
+            if (lane == 0) wpre[w] = __popcll(word);
         }
         __syncthreads();
+        if (wid == 0) {
+            int c = lane < nwords ? wpre[lane] : 0, x = c;
+            for (int o = 1; o < 64; o <<= 1) { int y = __shfl_up(x, o); if (lane >= o) x += y; }
+            if (lane < nwords) wpre[lane] = x - c;
+            if (lane == 63) s_nE = x;
+        }
+        __syncthreads();
+        for (int w = wid; w < nwords; w += T / 64) {
+            const int j = (w << 6) + lane;
+            const int rel = j < nA ? (int)(uint16_t)(Ap[j] - p16) : 0;
+            const bool bit = j < nA && (rel < relLE || rel >= relRE);
+            const unsigned long long word = __ballot(bit);
+            if (bit) E[wpre[w] + __popcll(word & ((1ull << lane) - 1ull))] = (uint32_t)j | ((uint32_t)rel << 16);
+        }
+        __syncthreads();
+        const int nE = s_nE;
+        STAMP(3);
 
-        /* ---- one output per thread ---- */
+        /* ---- one output per lane; the wave walks the edge list in lockstep ----
+         * qa: k-th valid sorted index  = k + #excluded edges at indices <= qa (fixpoint)
+         * qb: next valid index after qa = qa+1 + #excluded edges met at exactly qb      */
         const int64_t i = i0 + tid;
+        int64_t s = 0, e = 0;
+        win_bounds(i < n ? i : n - 1, n, W, s, e);
+        const int64_t lo = s > t0 ? s : t0;
+        const int64_t nobs = (i < i1 && e > lo) ? e - lo : 0;
+        const bool valid = nobs >= minp && nobs > 0;
+        const int xlo = (int)(lo - P0), xhi = (int)(e - P0);
+        int64_t k = 0;
+        double idxf = 0;
+        if (valid && nobs > 1) {
+            idxf = q * (double)(nobs - 1);
+            k = (int64_t)idxf;
+        }
+        /* excluded edges e_1 < e_2 < ... (sorted indices): the k-th valid index is
+         * qa = k + #{j : e_j - (j-1) <= k}, and e_j - (j-1) never decreases, so one
+         * pass with a running excluded-count jx is exact and can stop early.  Pure
+         * integer VALU (sign-bit tests); the edge arrives in an SGPR. */
+        int jx = 0, m = 0;
+        const int kk = valid ? (int)k : -(1 << 30);   /* invalid lanes never count */
+        for (int e0 = 0; e0 < nE; e0 += 64) {
+            const uint32_t mine = (e0 + lane < nE) ? E[e0 + lane] : 0xFFFFFFFFu;
+            const int sfirst = (int)(__builtin_amdgcn_readfirstlane((int)mine) & 0xFFFF);
+            if (!__ballot(sfirst - jx <= kk)) break;          /* no lane can count another edge */
+            const int cnt = nE - e0 < 64 ? nE - e0 : 64;
+            for (int u = 0; u < cnt; ++u) {
+                const uint32_t ent = (uint32_t)__builtin_amdgcn_readlane((int)mine, u);
+                const int sj = (int)(ent & 0xFFFFu), pj = (int)(ent >> 16);
+                const int ex = (int)((uint32_t)((pj - xlo) | (xhi - 1 - pj)) >> 31);
+                const int ok = 1 - (int)((uint32_t)(kk - sj + jx) >> 31);
+                m += ex & ok;
+                jx += ex;
+            }
+        }
+        const int qa = (int)k + m;
+        int qb = qa + 1;
+        if (valid && nobs > 1) {   /* next valid sorted index after qa: skip excluded positions */
+            for (;;) {
+                const int rel = (int)(uint16_t)(Ap[qb] - p16);
+                if (rel >= xlo && rel < xhi) break;
+                ++qb;
+            }
+        }
+        STAMP(4);
         if (i < i1) {
-            int64_t s, e;
-            win_bounds(i, n, W, s, e);
-            const int64_t lo = s > t0 ? s : t0;
-            const int64_t nobs = e > lo ? e - lo : 0;
             double res = __builtin_nan("");
-            if (nobs >= minp && nobs > 0) {
-                const int xlo = (int)(lo - P0), xhi = (int)(e - P0);
-                int64_t k;
-                double idxf = 0;
-                bool interp = false;
-                if (nobs == 1) {
-                    k = 0;
-                } else {
-                    idxf = q * (double)(nobs - 1);
-                    k = (int64_t)idxf;
-                    interp = (double)k != idxf;
-                }
-                /* walk the edge bitmap: first the k-th valid sorted index */
-                int qa = (int)k;
-                int w = 0;
-                unsigned long long bits = nwords > 0 ? ebits[0] : 0ull;
-                for (;;) {
-                    while (bits == 0ull && w + 1 < nwords) bits = ebits[++w];
-                    if (bits == 0ull) break;
-                    const int j = (w << 6) + __ffsll((long long)bits) - 1;
-                    if (j > qa) break;
-                    const int rel = (uint16_t)(Ap[j] - p16);
-                    if (rel < xlo || rel >= xhi) qa++;
-                    bits &= bits - 1ull;
-                }
+            if (valid) {
                 const double va = Av[qa];
-                if (!interp) {
-                    res = va;
-                } else {
-                    int qb = qa + 1;
-                    for (;;) {
-                        while (bits == 0ull && w + 1 < nwords) bits = ebits[++w];
-                        if (bits == 0ull) break;
-                        const int j = (w << 6) + __ffsll((long long)bits) - 1;
-                        if (j > qb) break;
-                        const int rel = (uint16_t)(Ap[j] - p16);
-                        if (j == qb && (rel < xlo || rel >= xhi)) qb++;
-                        bits &= bits - 1ull;
-                    }
+                if (nobs == 1 || (double)k == idxf) res = va;
+                else {
                     const double vb = Av[qb];
                     res = va + (vb - va) * (idxf - (double)k);
                 }
-                atomicMin(&s_first, (int)i);
-                atomicMax(&s_last, (int)i);
             }
             out[i] = res;
         }
+        {
+            const unsigned long long vm = __ballot(valid);
+            if (vm && lane == 0) {
+                atomicMin(&s_first, (int)(i0 + wid * 64 + __ffsll((long long)vm) - 1));
+                atomicMax(&s_last, (int)(i0 + wid * 64 + 63 - __clzll(vm)));
+            }
+        }
         __syncthreads();
+        STAMP(5);
     }
+    STAMP_FLUSH(A.stamps);
     /* ---- .bfill().ffill() ---- */
     const int first = s_first, last = s_last;
     if (last < 0) {
@@ -272,8 +378,8 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     for (int64_t i = last + 1 + tid; i < n; i += T) out[i] = vl;
 }
 
-template __global__ void k_rolling_quantile<256>(RollqArgs A);
-template __global__ void k_rolling_quantile<128>(RollqArgs A);
+template __global__ void k_rolling_quantile<256, 16>(RollqArgs A);
+template __global__ void k_rolling_quantile<256, 32>(RollqArgs A);
 
 /* ------------------------------------------------------------------------ */
 __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Run GPU steps in order on the gpurun box; stop at the first crash/timeout
+# (exit codes other than 0 = ok and 1 = ordinary test failure).
+set -u
+mkdir -p gpurun_out
+run() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    pytest) run pytest_gpu 1000 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
+    bench_native) run bench_native 600 python bench.py --steps 10 --warmup 2 --mode native ;;
+    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+    rocprof_native) run rocprof_native 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_native -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --mode native ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
