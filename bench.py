@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", default="reference", choices=["reference", "native"])
+    ap.add_argument("--mode", default="native", choices=["native", "reference"])
     ap.add_argument("--files", type=int, default=1024, help="recordings per GPU")
     ap.add_argument("--secs", type=float, default=60.0)
     ap.add_argument("--fs", type=int, default=44100)
@@ -45,8 +45,8 @@ def parse():
 def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, channels: int = 1) -> dict:
     """Algorithmic HBM bytes per launch of the dominant kernels."""
     if mode == "native":
-        # every PCM sample is read once (int16), the decimated output written once
-        return {"k_envelope_native": n_files * (n_frames * channels * 2 + nd * 8)}
+        # every PCM sample is read once (int16): SURVEY.md §8(d)
+        return {"k_native_blocks": n_files * n_frames * channels * 2}
     # reference: the picked int16 samples, y kept in scratch (written fwd, rewritten bwd, read twice),
     # env written once
     return {"k_envelope_ref": n_files * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8),

@@ -27,6 +27,11 @@ struct bpmx_ctx {
     int device = 0;
     std::map<std::string, std::pair<void *, size_t>> bufs;
     std::vector<int64_t> g_key;   /* geometry of the last upload */
+    /* native-mode block-state tables (host copies back the async uploads) */
+    std::vector<int64_t> nat_key;
+    std::vector<double> nat_tab;
+    std::vector<int64_t> nat_boff;
+    bool nat_tab_dirty = false;
     bool prof = false;
     struct Rec { std::string name; hipEvent_t a, b; };
     std::vector<Rec> recs;

@@ -135,3 +135,23 @@ def test_dropin_functions(det, tmp_path):
         short = tmp_path / "short.wav"
         wavfile.write(str(short), 44100, O.synth(1, 146 * 15, 44100, 1))
         B.preprocess_audio(str(short), params, str(tmp_path))
+
+
+@pytest.mark.parametrize("name", G.names(kind="pcm", mode="native"))
+def test_native_mode_golden(det, name):
+    """north_star ordering (sosfiltfilt @ fs -> [::ds] -> |hilbert| -> rolling mean):
+    envelope within 1e-9 relative of the scipy composition, indices exact."""
+    g = G.load(name)
+    r = det.run_host([g["pcm"]], int(g["fs"]), g["params"], mode="native", want_y=True)[0]
+    assert r["sr"] == int(g["sr"])
+    scale = np.max(np.abs(g["y"]))
+    assert np.max(np.abs(r["y"] - g["y"])) <= 1e-9 * scale
+    _check_file(r, g, exact_env=False)
+
+
+def test_native_ragged_batch(det):
+    names = ["nat_44k_60s_mono", "nat_44k_40s_clicks"]
+    gs = [G.load(n) for n in names]
+    res = det.run_host([g["pcm"] for g in gs], 44100, G.BASE_PARAMS, mode="native")
+    for r, g in zip(res, gs):
+        _check_file(r, g, exact_env=False)

@@ -17,10 +17,10 @@ for step in "$@"; do
   case $step in
     pytest) run pytest_gpu 1000 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
-    bench_native) run bench_native 600 python bench.py --steps 10 --warmup 2 --mode native ;;
+    bench) run bench 600 python bench.py ;;
+    bench_ref) run bench_ref 600 python bench.py --steps 10 --warmup 2 --mode reference ;;
     rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
-    rocprof_native) run rocprof_native 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_native -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --mode native ;;
+    rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --mode reference ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step"; exit 2 ;;
