@@ -165,7 +165,7 @@ def main():
         kernels = {k: {"launches": c, "avg_ms": round(t / c, 4)} for k, (c, t) in sorted(prof.items())}
         cpu = None
         if not args.no_cpu and args.cpu_files != 0:
-            nfc = args.cpu_files if args.cpu_files > 0 else (256 if args.mode == "reference" else 64)
+            nfc = args.cpu_files if args.cpu_files > 0 else min(F, 1024)
             cpu = cpu_baseline(args.mode, fs, n, nfc, params)
         line = {
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,

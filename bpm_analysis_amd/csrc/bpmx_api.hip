@@ -235,9 +235,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     geo.insert(geo.end(), foff.begin(), foff.end());
     geo.insert(geo.end(), doff.begin(), doff.end());
     geo.insert(geo.end(), boff.begin(), boff.end());
-    int64_t *dgeo = (int64_t *)ctx->buf("geo", geo.size() * 8, &rc);
-    int32_t *di = (int32_t *)ctx->buf("geo_i", (size_t)F * 4 * 8, &rc);
+    bool g1 = false, g2 = false;
+    int64_t *dgeo = (int64_t *)ctx->buf("geo", geo.size() * 8, &rc, &g1);
+    int32_t *di = (int32_t *)ctx->buf("geo_i", (size_t)F * 4 * 8, &rc, &g2);
     if (rc != BPMX_OK) return rc;
+    if (g1 || g2) ctx->g_key.clear();
     std::vector<int64_t> key = geo;
     key.push_back(F);
     key.push_back(do_env);

@@ -31,6 +31,9 @@ struct bpmx_ctx {
     std::vector<int64_t> nat_key;
     std::vector<double> nat_tab;
     std::vector<int64_t> nat_boff;
+    std::vector<int64_t> nat_tkey, nat_tdoff;   /* tile-list geometry key */
+    std::vector<char> nat_tiles;                /* host copy of the tile list */
+    bool nat_tiles_dirty = false;
     bool nat_tab_dirty = false;
     bool prof = false;
     struct Rec { std::string name; hipEvent_t a, b; };
@@ -38,10 +41,13 @@ struct bpmx_ctx {
     std::vector<hipEvent_t> pool;
     std::map<std::string, std::pair<long, double>> totals;
 
-    /* grow-only device scratch */
-    void *buf(const std::string &name, size_t bytes, int *rc) {
+    /* grow-only device scratch; *grew (optional) reports a fresh allocation,
+     * whose contents the caller must re-upload */
+    void *buf(const std::string &name, size_t bytes, int *rc, bool *grew = nullptr) {
         auto &e = bufs[name];
+        if (grew) *grew = false;
         if (e.second < bytes) {
+            if (grew) *grew = true;
             if (e.first) (void)hipFree(e.first);
             e.first = nullptr;
             e.second = 0;

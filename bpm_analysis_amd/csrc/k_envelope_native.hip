@@ -41,10 +41,14 @@ namespace bpmx {
 /* table layout (native_tables.pack) */
 enum { TB_A = 0, TB_B = 16, TB_C = 20, TB_D = 24, TB_M = 25, TB_P = 41, TB_ZI = 57, TB_COEF = 64 };
 
+struct NatTile;
 struct NatBlockArgs {
     const void *pcm;
     const int64_t *foff, *boff;   /* frame offsets, block offsets (blocks = Nd-1 per file) */
     const int64_t *boffp;         /* padded per-file block storage: 64 * ceil(nb/64) entries */
+    const struct NatTile *tiles;  /* int16 mono path: tile list */
+    int64_t n_tiles, total;       /* tiles; samples in pcm */
+    int bt;                       /* blocks per tile */
     const int32_t *active;
     int32_t n_files, channels, ds;
     const double *tab;
@@ -89,62 +93,101 @@ __device__ __forceinline__ double nat_frame(const void *__restrict__ pcm, int ch
     return frame_value(pcm, DT, ch, frame);
 }
 
-/* int16 mono fast path: no LDS — each lane streams its own block (ds+1
- * samples) with dword-x4 loads straight from HBM/L2, so occupancy is set by
- * registers alone and every sample is fetched from HBM once (the 8-sample
- * chunks of one lane reuse the same cache lines). */
-constexpr int NB_T = 256;
-__global__ __launch_bounds__(NB_T) void k_native_blocks_i16(NatBlockArgs A) {
-    const int f = blockIdx.y;
-    if (f >= A.n_files || !A.active[f]) return;
-    const int64_t nb = A.boff[f + 1] - A.boff[f];
-    const int64_t j = (int64_t)blockIdx.x * NB_T + threadIdx.x;
-    if (j >= nb) return;
-    const int ds = A.ds;
-    const int64_t R = (nb + 63) >> 6;
-    const int64_t e = A.boffp[f] + (j % R) * 64 + j / R;          /* [t][lane] layout for k_native_scan */
-    const int16_t *xb = (const int16_t *)A.pcm + A.foff[f] + j * ds;
-    const uint32_t *wb = (const uint32_t *)((uintptr_t)xb & ~(uintptr_t)3);
-    const bool odd = ((uintptr_t)xb & 2) != 0;
-    const double *__restrict__ coef = A.tab + TB_COEF;
-    double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-    auto acc = [&](double xv, const double *c) {
-        u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
-        u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
-        v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
-        v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
+/* int16 mono fast path.  Persistent single-wave workgroups walk a list of
+ * tiles (up to 64 consecutive blocks of one file).  A tile's samples arrive
+ * with coalesced 16-byte loads into registers — issued one tile AHEAD, so
+ * HBM latency hides behind the current tile's FMAs — then go through LDS,
+ * where lane b reads block b's ds+1 samples (lane stride ds/2 dwords: odd for
+ * the usual ds, conflict-free).  The 8 coefficients of each sample are
+ * wave-uniform scalar loads. */
+constexpr int NB_RCH = 20;              /* 16-byte chunks per lane per tile: <= 10240 samples */
+struct NatTile {
+    int64_t s0;                         /* first sample of the tile (index into pcm) */
+    int64_t ebase;                      /* boffp[f] */
+    int32_t j0, nb;                     /* first block, blocks of the file */
+};
+
+__device__ __forceinline__ double nat_lo16(uint32_t w) { return (double)(int)(int16_t)(w & 0xFFFFu); }
+__device__ __forceinline__ double nat_hi16(uint32_t w) { return (double)((int)w >> 16); }
+
+typedef uint32_t nat_u4 __attribute__((ext_vector_type(4)));
+/* `coef` is passed separately as __restrict__ so its loads become scalar
+ * (wave-uniform) loads: the compiler must know the uv stores cannot alias it */
+__global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const double *__restrict__ coef) {
+    typedef nat_u4 u4;
+    __shared__ u4 tile[NB_RCH * 64];
+    const int lane = threadIdx.x;
+    const int16_t *pcm = (const int16_t *)A.pcm;
+    const int64_t total = A.total;
+    const int ds = A.ds, bt = A.bt;
+    const int nch = (7 + bt * ds + 1 + 7) >> 3;           /* chunks a tile may touch */
+    auto issue = [&](int64_t t, u4 *reg, int &off) {
+        const int64_t s0 = A.tiles[t].s0;
+        const int64_t a0 = s0 & ~(int64_t)7;
+        off = (int)(s0 - a0);
+#pragma unroll
+        for (int r = 0; r < NB_RCH; ++r) {
+            const int q = r * 64 + lane;
+            const int64_t c = a0 + (int64_t)q * 8;
+            if (q < nch && c + 8 <= total) __builtin_memcpy(&reg[r], pcm + c, 16);
+            else reg[r] = u4{0, 0, 0, 0};      /* a partial last chunk is patched in LDS */
+        }
     };
-    const int nfull = (ds + 1) >> 3;       /* chunks of 8 samples; row ds has F = 0 */
-    for (int c = 0; c < nfull; ++c) {
-        const uint32_t *wp = wb + c * 4;
-        uint32_t w0, w1, w2, w3;
+    u4 reg[NB_RCH];
+    int off = 0;
+    int64_t t = blockIdx.x;
+    if (t < A.n_tiles) issue(t, reg, off);
+    while (t < A.n_tiles) {
+        const NatTile tl = A.tiles[t];
+#pragma unroll
+        for (int r = 0; r < NB_RCH; ++r) tile[r * 64 + lane] = reg[r];
+        const int coff = off;
         {
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            u4 w;
-            __builtin_memcpy(&w, wp, 16);
-            w0 = w.x; w1 = w.y; w2 = w.z; w3 = w.w;
+            const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
+            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))
+                ((int16_t *)tile)[tail0 - a0 + lane] = pcm[tail0 + lane];
         }
-        if (odd) {
-            const uint32_t w4 = wp[4];
-            w0 = __builtin_amdgcn_alignbit(w1, w0, 16);
-            w1 = __builtin_amdgcn_alignbit(w2, w1, 16);
-            w2 = __builtin_amdgcn_alignbit(w3, w2, 16);
-            w3 = __builtin_amdgcn_alignbit(w4, w3, 16);
+        __syncthreads();
+        const int64_t tn = t + gridDim.x;
+        if (tn < A.n_tiles) issue(tn, reg, off);
+        const int j = tl.j0 + lane;
+        if (lane < bt && j < tl.nb) {
+            const int base = coff + lane * ds;                        /* halfword index in the tile */
+            const uint32_t *wp = (const uint32_t *)tile + (base >> 1);
+            const uint32_t sh = (base & 1) ? 16u : 0u;
+            double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+            auto acc = [&](double xv, const double *c) {
+                u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
+                u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
+                v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
+                v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
+            };
+            const int L = ds + 1;                                    /* row ds has F = 0 */
+            int i = 0;
+            for (; i + 8 <= L; i += 8) {
+                const uint32_t *p = wp + i / 2;
+                const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+                const uint32_t d0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+                const uint32_t d1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+                const uint32_t d2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+                const uint32_t d3 = __builtin_amdgcn_alignbit(w4, w3, sh);
+                const double *cr = coef + (int64_t)i * 8;
+                acc(nat_lo16(d0), cr + 0);  acc(nat_hi16(d0), cr + 8);
+                acc(nat_lo16(d1), cr + 16); acc(nat_hi16(d1), cr + 24);
+                acc(nat_lo16(d2), cr + 32); acc(nat_hi16(d2), cr + 40);
+                acc(nat_lo16(d3), cr + 48); acc(nat_hi16(d3), cr + 56);
+            }
+            const int16_t *th = (const int16_t *)tile;
+            for (; i < L; ++i) acc((double)th[base + i], coef + (int64_t)i * 8);
+            const uint32_t R = ((uint32_t)tl.nb + 63u) >> 6;
+            const int64_t e = tl.ebase + (int64_t)((uint32_t)j % R) * 64 + (uint32_t)j / R;
+            double2 *o = (double2 *)(A.uv + e * 8);
+            o[0] = make_double2(u0, u1); o[1] = make_double2(u2, u3);
+            o[2] = make_double2(v0, v1); o[3] = make_double2(v2, v3);
         }
-        const double *cr = coef + (int64_t)c * 64;
-        acc((double)(int16_t)(w0 & 0xFFFFu), cr + 0);
-        acc((double)(int16_t)(w0 >> 16), cr + 8);
-        acc((double)(int16_t)(w1 & 0xFFFFu), cr + 16);
-        acc((double)(int16_t)(w1 >> 16), cr + 24);
-        acc((double)(int16_t)(w2 & 0xFFFFu), cr + 32);
-        acc((double)(int16_t)(w2 >> 16), cr + 40);
-        acc((double)(int16_t)(w3 & 0xFFFFu), cr + 48);
-        acc((double)(int16_t)(w3 >> 16), cr + 56);
+        __syncthreads();
+        t = tn;
     }
-    for (int i = nfull * 8; i <= ds; ++i) acc((double)xb[i], coef + (int64_t)i * 8);
-    double2 *o = (double2 *)(A.uv + e * 8);
-    o[0] = make_double2(u0, u1); o[1] = make_double2(u2, u3);
-    o[2] = make_double2(v0, v1); o[3] = make_double2(v2, v3);
 }
 
 /* generic path (other sample formats, multi-channel): f64 tile, 32 blocks per group */
@@ -618,7 +661,9 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         ctx->nat_key = key;
         ctx->nat_tab_dirty = true;
     }
-    double *d_tab = (double *)ctx->buf("nat_tab", ctx->nat_tab.size() * 8, &rc);
+    bool grew = false;
+    double *d_tab = (double *)ctx->buf("nat_tab", ctx->nat_tab.size() * 8, &rc, &grew);
+    if (grew) ctx->nat_tab_dirty = true;
     std::vector<int64_t> boff(F + 1, 0);
     for (int f = 0; f < F; ++f) {
         const int64_t nd = doff[f + 1] - doff[f];
@@ -627,7 +672,8 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     std::vector<int64_t> boffp(F + 1, 0);
     for (int f = 0; f < F; ++f) boffp[f + 1] = boffp[f] + ((boff[f + 1] - boff[f] + 63) / 64) * 64;
     const int64_t sum_blocks = boffp[F];
-    int64_t *d_boff2 = (int64_t *)ctx->buf("nat_boff", (size_t)(F + 1) * 16, &rc);
+    int64_t *d_boff2 = (int64_t *)ctx->buf("nat_boff", (size_t)(F + 1) * 16, &rc, &grew);
+    if (grew) ctx->nat_boff.clear();
     if (rc != BPMX_OK) return rc;
     if (ctx->nat_tab_dirty) {
         HIP_TRY(hipMemcpyAsync(d_tab, ctx->nat_tab.data(), ctx->nat_tab.size() * 8, hipMemcpyHostToDevice, s));
@@ -652,10 +698,42 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         NatBlockArgs a;
         a.pcm = B->pcm; a.foff = d_foff; a.boff = d_boff2; a.boffp = d_boffp; a.active = d_active; a.n_files = F;
         a.channels = P->channels; a.ds = ds; a.tab = d_tab; a.uv = uv;
+        const bool fast = P->dtype == BPMX_DT_I16 && P->channels == 1 && ((uintptr_t)B->pcm & 15) == 0;
         if (maxnb > 0) {
-            if (P->dtype == BPMX_DT_I16 && P->channels == 1) {
-                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16,
-                       dim3((unsigned)((maxnb + NB_T - 1) / NB_T), F), dim3(NB_T), 0, s, a);
+            if (fast) {
+                const int bt = std::min(64, (NB_RCH * 512 - 16) / ds);
+                std::vector<int64_t> tk(3 + F);
+                tk[0] = bt; tk[1] = F; tk[2] = foff[F];
+                for (int f = 0; f < F; ++f) tk[3 + f] = foff[f];
+                if (tk != ctx->nat_tkey || doff != ctx->nat_tdoff) {
+                    std::vector<NatTile> tv;
+                    for (int f = 0; f < F; ++f) {
+                        const int64_t nd = doff[f + 1] - doff[f];
+                        if (nd <= 15) continue;                      /* inactive (filtfilt would raise) */
+                        const int64_t nb = nd - 1;
+                        for (int64_t j0 = 0; j0 < nb; j0 += bt)
+                            tv.push_back(NatTile{foff[f] + j0 * ds, boffp[f], (int32_t)j0, (int32_t)nb});
+                    }
+                    ctx->nat_tiles.resize(tv.size() * sizeof(NatTile));
+                    std::memcpy(ctx->nat_tiles.data(), tv.data(), ctx->nat_tiles.size());
+                    ctx->nat_tkey = tk;
+                    ctx->nat_tdoff = doff;
+                    ctx->nat_tiles_dirty = true;
+                }
+                const int64_t nt = (int64_t)(ctx->nat_tiles.size() / sizeof(NatTile));
+                NatTile *d_tiles =
+                    (NatTile *)ctx->buf("nat_tiles", std::max<size_t>(ctx->nat_tiles.size(), 64), &rc, &grew);
+                if (rc != BPMX_OK) return rc;
+                if (grew) ctx->nat_tiles_dirty = true;
+                if (ctx->nat_tiles_dirty) {
+                    HIP_TRY(hipMemcpyAsync(d_tiles, ctx->nat_tiles.data(), ctx->nat_tiles.size(),
+                                           hipMemcpyHostToDevice, s));
+                    ctx->nat_tiles_dirty = false;
+                }
+                a.tiles = d_tiles; a.n_tiles = nt; a.total = foff[F]; a.bt = bt;
+                const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(nt, 1), 256 * 8);
+                if (nt > 0) LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16, dim3(grid), dim3(64), 0, s, a,
+                                   (const double *)(d_tab + TB_COEF));
             } else {
                 const dim3 g((unsigned)((maxnb + 31) / 32), F), b(64);
                 const size_t lds = ((size_t)32 * ds + 1) * 8;
