@@ -39,18 +39,51 @@ def parse():
     ap.add_argument("--fs", type=int, default=44100)
     ap.add_argument("--cpu-files", type=int, default=-1, help="CPU baseline sample size (-1: auto, 0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pcie-steps", type=int, default=3, help="steps of the PCIe-inclusive side measurement (0: skip)")
     return ap.parse_args()
 
 
-def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, channels: int = 1) -> dict:
-    """Algorithmic HBM bytes per launch of the dominant kernels."""
+def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, channels: int = 1) -> dict:
+    """Algorithmic HBM bytes per launch of each kernel: the
+    bytes the algorithm must move, not what the implementation happens to move."""
+    F = n_files
+    nb = nd - 1
+    half = nd // 2 + 1
+    common = {
+        "k_quantile": F * nd * 8,                          # env read once
+        "k_block_stats": F * nd * 8,
+        "k_find_peaks[troughs]": F * nd * 8,
+        "k_find_peaks[peaks]": F * nd * 16,                # env + floor
+        "k_interp": F * nd * 8,                            # dense written once
+        "k_rolling_quantile": F * nd * 16,                 # dense in, quantile out
+        "k_sanitize": 0, "k_floor_final": F * nd * 8,
+    }
     if mode == "native":
-        # every PCM sample is read once (int16): SURVEY.md §8(d)
-        return {"k_native_blocks": n_files * n_frames * channels * 2}
-    # reference: the picked int16 samples, y kept in scratch (written fwd, rewritten bwd, read twice),
-    # env written once
-    return {"k_envelope_ref": n_files * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8),
-            "k_rolling_quantile": n_files * (nd * 8 + nd * 8)}
+        return dict(common, **{
+            "k_native_blocks": F * n_frames * channels * 2,      # every PCM sample read once (SURVEY 8(d))
+            "k_native_scan": F * (nb * (64 + 32 + 32) + nd * (8 + 2 * channels)),
+            "rocfft_r2c": F * (nd * 8 + half * 16),
+            "k_hilbert_weights": F * half * 16 * 2,
+            "rocfft_c2c_inv": F * nd * 16 * 2,
+            "k_native_env": F * nd * (16 + 8),
+        })
+    # reference: the picked samples, y kept in scratch (written fwd, rewritten bwd, read twice), env written once
+    return dict(common, **{"k_envelope_ref": F * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8)})
+
+
+def pmc_traffic(mode: str, kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 calibration), or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{mode}.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(mode: str, fs: int, n_frames: int, n_files: int, params: dict) -> dict:
@@ -89,6 +122,28 @@ def cpu_baseline(mode: str, fs: int, n_frames: int, n_files: int, params: dict) 
                       f"oracle/bpmx_oracle.c on {cores} threads of {cpu}; {dt:.2f} s wall"}
 
 
+def shard_seed0(rank: int, files_per_gpu: int) -> int:
+    """Weak scaling: rank r synthesises files r*F .. r*F+F-1 (disjoint shards)."""
+    return rank * files_per_gpu
+
+
+def reduce_results(elapsed: float, n_peaks, world: int, rank: int):
+    """Max wall time over ranks, and the final result gather: every shard's
+    per-file raw-peak counts to rank 0 (RCCL on the GPU box, gloo in the CPU
+    tests).  The only collectives of the job."""
+    import torch
+    import torch.distributed as dist
+    if world <= 1:
+        return elapsed, int(n_peaks.sum())
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=n_peaks.device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    counts = n_peaks.clone()
+    gathered = [torch.empty_like(counts) for _ in range(world)] if rank == 0 else None
+    dist.gather(counts, gathered, dst=0)
+    total = int(sum(int(g.sum()) for g in gathered)) if rank == 0 else 0
+    return float(tt.item()), total
+
+
 def main():
     args = parse()
     import torch
@@ -112,7 +167,7 @@ def main():
     n = int(round(args.secs * fs))
     d = design(fs, params, log=False)
     fo = np.arange(F + 1, dtype=np.int64) * n
-    pcm = det.synth(fo, fs, 1, seed0=rank * F)
+    pcm = det.synth(fo, fs, 1, seed0=shard_seed0(rank, F))
     out = det.alloc(fo, d.ds, d.sr)
     nd = -(-n // d.ds)
 
@@ -135,23 +190,33 @@ def main():
     t1 = time.perf_counter()
     det.profile(False)
     prof = det.profile_read()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=det.device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        # final result gather (RCCL): per-file raw-peak counts of every shard to rank 0
-        counts = out.n_peaks.clone()
-        gathered = [torch.empty_like(counts) for _ in range(world)] if rank == 0 else None
-        dist.gather(counts, gathered, dst=0)
-        total_peaks = int(sum(int(g.sum()) for g in gathered)) if rank == 0 else 0
-    else:
-        total_peaks = int(out.n_peaks.sum())
+    elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
+
+    # PCIe-inclusive rate: the same step with the PCM handed over in
+    # pinned host memory and copied to HBM inside the timed region.  Reported
+    # beside `value`, never as it.
+    pcie = None
+    if args.pcie_steps > 0:
+        host = pcm.cpu().pin_memory()
+        stream = torch.cuda.current_stream(det.device)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for _ in range(args.pcie_steps):
+            pcm.copy_(host, non_blocking=True)
+            step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t2) / args.pcie_steps
+        pcie = {"value": F * n / dt, "unit": "audio-samples/s", "ms_per_step": dt * 1e3,
+                "h2d_bytes_per_step": F * n * 2, "steps": args.pcie_steps, "per_gpu": True}
+        del host, stream
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         value = world * F * n / (elapsed / args.steps)
-        abytes = algorithmic_bytes(args.mode, F, n, nd)
+        abytes = algorithmic_bytes(args.mode, F, n, nd, d.ds)
+        workload = (f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
+                    f"(filter+envelope+noise floor+raw peaks)")
+        # dominant kernel = the largest share of the step (summed over its launches)
         timed = {k: v for k, v in prof.items() if k in abytes}
         dom = max(timed, key=lambda k: timed[k][1]) if timed else None
         roof = None
@@ -160,9 +225,18 @@ def main():
             avg_s = tot / cnt / 1e3
             ach = abytes[dom] / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom,
-                    "kernel_avg_ms": round(avg_s * 1e3, 4)}
-        kernels = {k: {"launches": c, "avg_ms": round(t / c, 4)} for k, (c, t) in sorted(prof.items())}
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(args.mode, dom, workload),
+                    "kernel": dom, "kernel_avg_ms": round(avg_s * 1e3, 4),
+                    "algorithmic_bytes_per_launch": abytes[dom]}
+        kernels = {}
+        for k, (c, t) in sorted(prof.items()):
+            kernels[k] = {"launches": c, "avg_ms": round(t / c, 4), "share": round(t / (elapsed * 1e3), 4)}
+            if abytes.get(k):
+                kernels[k]["algo_GBps"] = round(abytes[k] / (t / c / 1e3) / 1e9, 1)
+        # whole-step view of the north-star roofline: PCM bytes (read once) / step time
+        step_bytes = F * n * 2
+        pipeline = {"hbm_bytes_per_step": step_bytes, "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
+                    "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
         cpu = None
         if not args.no_cpu and args.cpu_files != 0:
             nfc = args.cpu_files if args.cpu_files > 0 else min(F, 1024)
@@ -171,13 +245,12 @@ def main():
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
-                                   f"(filter+envelope+noise floor+raw peaks)",
+            "config": {"workload": workload,
                        "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
                        "parallelism": f"file-sharded x{world}"},
             "roofline": roof, "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
-            "kernels": kernels, "total_raw_peaks": total_peaks,
+            "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
         }
         print(json.dumps(line))
     if world > 1:

@@ -46,9 +46,15 @@ def _write_debug_wav(path: str, sr: int, y: np.ndarray) -> None:
         wavfile.write(path, sr, np.int16(y / np.max(np.abs(y)) * 32767))
 
 
-def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: str = "reference",
+def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: str = None,
                      device: int = 0) -> Tuple[np.ndarray, int]:
-    """Reads, filters, and prepares the audio envelope for analysis (on the GPU)."""
+    """Reads, filters, and prepares the audio envelope for analysis (on the GPU).
+
+    ``mode`` (or ``params["bpmx_mode"]`` when called through the reference's
+    unchanged ``analyze_wav_file``): "reference" (default, bit-exact with the
+    shipped pipeline) or "native" (sosfiltfilt at fs -> decimate -> |hilbert|)."""
+    if mode is None:
+        mode = params.get("bpmx_mode", "reference")
     save_debug_file = params["save_filtered_wav"]
     sample_rate, audio = _read_wav(file_path)
     d = design(sample_rate, params)

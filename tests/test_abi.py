@@ -59,3 +59,26 @@ def test_create_without_gpu_fails_cleanly():
     rc = N.load().bpmx_create(0, ctypes.byref(c))
     assert rc == N.E_NODEV
     assert b"device" in N.load().bpmx_last_error()
+
+
+def test_reference_side_stub_matches_package():
+    """tools/ctypes_stub.py declares the same C structs and
+    derives byte-identical bpmx_params to the package's host code."""
+    import ctypes
+    import importlib.util
+    import os
+
+    from bpm_analysis_amd import DEFAULT_PARAMS
+    from bpm_analysis_amd import _native as N
+    from bpm_analysis_amd.design import design, make_params
+    spec = importlib.util.spec_from_file_location("ctypes_stub", os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "ctypes_stub.py"))
+    stub = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(stub)
+    for a, b in [(stub.Params, N.Params), (stub.Batch, N.Batch), (stub.Out, N.Out)]:
+        assert ctypes.sizeof(a) == ctypes.sizeof(b)
+        assert [f[0] for f in a._fields_] == [f[0] for f in b._fields_]
+    for fs in (44100, 48000, 96000, 22050):
+        p1 = stub.make_params(fs, DEFAULT_PARAMS)
+        p2 = make_params(design(fs, DEFAULT_PARAMS, log=False), DEFAULT_PARAMS, 0, 7, 1, 1)
+        assert bytes(p1) == bytes(p2)

@@ -1,0 +1,55 @@
+"""Multi-rank path of bench.py on CPU (gloo, world size 2): disjoint file
+shards, max-over-ranks timing and the rank-0 gather of per-file results."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    counts = torch.arange(4, dtype=torch.int32) + 10 * rank      # per-file peak counts of this shard
+    elapsed, total = bench.reduce_results(1.0 + rank, counts, world, rank)
+    q.put((rank, elapsed, total, bench.shard_seed0(rank, 4)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_and_max_time():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, e0, t0, s0), (r1, e1, t1, s1) = res
+    assert e0 == e1 == 2.0                        # max over ranks
+    assert t0 == (0 + 1 + 2 + 3) + (10 + 11 + 12 + 13) and t1 == 0
+    assert (s0, s1) == (0, 4)                     # disjoint synthetic shards
+
+
+def test_single_rank_passthrough():
+    import bench
+    e, t = bench.reduce_results(3.5, torch.tensor([1, 2, 3]), 1, 0)
+    assert e == 3.5 and t == 6
+
+
+def test_algorithmic_bytes_native_reads_pcm_once():
+    import bench
+    ab = bench.algorithmic_bytes("native", 1024, 2646000, 18124, 146)
+    assert ab["k_native_blocks"] == 1024 * 2646000 * 2
+    assert set(ab) >= {"k_rolling_quantile", "k_native_scan", "rocfft_r2c"}

@@ -176,3 +176,18 @@ def test_native_tile_geometries(det, fs, lens, shift):
         scale = np.max(np.abs(o["y"]))
         assert np.max(np.abs(h["y"] - o["y"])) <= 1e-9 * scale
         _check_file(h, o, exact_env=False)
+
+
+def test_reference_side_ctypes_stub():
+    """INTEGRATION.md's torch-free ctypes binding of the C ABI, on a golden."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ctypes_stub", os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "ctypes_stub.py"))
+    stub = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(stub)
+    import bpm_analysis_amd as B
+    g = G.load("ref_44k_60s_mono")
+    env, floor, tr, pk, sr = stub.analyze(g["pcm"], int(g["fs"]), dict(B.DEFAULT_PARAMS))
+    assert sr == int(g["sr"])
+    assert _same(env, g["env"]) and _same(floor, g["floor"])
+    assert _same(tr, g["troughs"]) and _same(pk, g["peaks"])

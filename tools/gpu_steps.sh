@@ -23,6 +23,8 @@ for step in "$@"; do
     rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --mode reference ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --mode reference ;;
+    pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --mode reference ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
