@@ -19,6 +19,7 @@ DT_U8, DT_I16, DT_I32, DT_F32, DT_F64 = 0, 1, 2, 3, 4
 MODE_REFERENCE, MODE_NATIVE = 0, 1
 STAGE_ENVELOPE, STAGE_FLOOR, STAGE_PEAKS, STAGE_ALL = 1, 2, 4, 7
 F_STATIC_FLOOR, F_DRAFT_FLOOR, F_NAN_FLOOR, F_TOO_SHORT = 1, 2, 4, 8
+OPT_ROLLQ_MERGE = 1
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",
@@ -29,7 +30,7 @@ class Params(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("stages", ctypes.c_int32), ("dtype", ctypes.c_int32),
                 ("channels", ctypes.c_int32), ("fs", ctypes.c_int32), ("ds", ctypes.c_int32),
                 ("sr", ctypes.c_int32), ("env_window", ctypes.c_int32), ("distance", ctypes.c_int32),
-                ("noise_window", ctypes.c_int32), ("min_periods", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("noise_window", ctypes.c_int32), ("min_periods", ctypes.c_int32), ("options", ctypes.c_int32),
                 ("trough_prom_q", ctypes.c_double), ("peak_prom_q", ctypes.c_double),
                 ("noise_floor_q", ctypes.c_double), ("fallback_q", ctypes.c_double),
                 ("reject_mult", ctypes.c_double),

@@ -336,14 +336,27 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         const int64_t W = P->noise_window;
         const int cap = (int)((W + RQ_T - 1 + 63) / 64 * 64);
         const size_t lds = rollq_lds_bytes(RQ_T, cap);
-        if (cap > 32 * RQ_T || W + RQ_T >= 65000)
+        /* wavelet-matrix kernel for recordings that fit its LDS budget; the
+         * sorted-union kernel for longer ones (or when forced) */
+        const bool use_wm = !(P->options & BPMX_OPT_ROLLQ_MERGE);
+        const bool need_merge = !use_wm || maxnd > WM_MMAX;
+        if (need_merge && (cap > 32 * RQ_T || W + RQ_T >= 65000))
             return fail(BPMX_E_LIMIT, "noise window of " + std::to_string(W) +
                                           " samples exceeds the rolling-quantile kernel (max 7800)");
+        double *wm_sorted = use_wm ? (double *)ctx->buf("wm_sorted", (size_t)sumnd * 8, &rc) : nullptr;
+        if (rc != BPMX_OK) return rc;
+        const size_t wm_lds = wm_lds_bytes(std::min<int64_t>(maxnd, WM_MMAX));
         auto rollq = [&](const int32_t *run, const int64_t *tr, double *outp, int32_t *allnan) -> int {
             RollqArgs a;
             a.dense = dense; a.doff = d_doff; a.troughs = tr; a.run = run; a.n_files = F;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
-            a.out = outp; a.allnan = allnan;
+            a.out = outp; a.allnan = allnan; a.wm_max = use_wm ? WM_MMAX : 0;
+            if (use_wm) {
+                (void)hipFuncSetAttribute((const void *)k_rollq_wm, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)wm_lds);
+                LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm, dim3(F), dim3(WM_T), wm_lds, s, a, wm_sorted);
+            }
+            if (!need_merge) return BPMX_OK;
             if (cap <= 16 * RQ_T) {
                 (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 16>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -80,6 +80,7 @@ struct RollqArgs {
     double q;
     double *out;
     int32_t *allnan;         /* [F] */
+    int32_t wm_max;          /* k_rolling_quantile skips files with n <= wm_max (k_rollq_wm took them) */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -130,6 +131,22 @@ __global__ void k_sanitize(SanitizeArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);
+
+/* wavelet-matrix rolling quantile (k_rollq_wm.hip): one 1024-thread workgroup
+ * per recording of <= WM_MMAX decimated samples */
+constexpr int WM_T = 1024;
+constexpr int WM_ITEMS = 18;                 /* 16-bit positions; LDS ~156 KB at the maximum */
+constexpr int WM_MMAX = WM_T * WM_ITEMS;     /* 18432 decimated samples (61 s at 302 Hz) */
+__host__ __device__ inline size_t wm_lds_bytes(int64_t nmax) {
+    const int64_t m = nmax < 1 ? 1 : nmax;
+    const int64_t L = m > 1 ? 64 - __builtin_clzll((unsigned long long)(m - 1)) : 1;
+    const int64_t NW = (m + 63) / 64;
+    const int64_t m8 = (m + 7) & ~7LL;
+    const int64_t sort_b = 8 * m8 + (int64_t)(WM_T / 64) * 128 * 4;   /* pos x2, key halves, counters */
+    const int64_t wm_b = 4 * m8 + L * (2 * NW + 1) * 8;               /* sequences x2, levels */
+    return (size_t)(sort_b > wm_b ? sort_b : wm_b);
+}
+__global__ void k_rollq_wm(RollqArgs A, double *sorted_scratch);
 
 }  // namespace bpmx
 

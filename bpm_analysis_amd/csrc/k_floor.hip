@@ -27,28 +27,7 @@
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 
-/* Optional in-kernel phase timing (tools/kbench.hip builds with -DBPMX_STAMPS;
- * the library never does): thread 0 accumulates s_memtime deltas per phase. */
-#ifdef BPMX_STAMPS
-#define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(k)                                                                  \
-    do {                                                                          \
-        if (threadIdx.x == 0) {                                                   \
-            unsigned long long _t = __builtin_amdgcn_s_memtime();                 \
-            _st_acc[k] += _t - _st_t;                                             \
-            _st_t = _t;                                                           \
-        }                                                                         \
-    } while (0)
-#define STAMP_FLUSH(ptr)                                                          \
-    do {                                                                          \
-        if (threadIdx.x == 0 && (ptr))                                            \
-            for (int _k = 0; _k < 8; ++_k) (ptr)[blockIdx.x * 8 + _k] = _st_acc[_k]; \
-    } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(k) do {} while (0)
-#define STAMP_FLUSH(ptr) do {} while (0)
-#endif
+#include "bpmx_stamps.h"
 
 namespace bpmx {
 
@@ -103,6 +82,7 @@ template <int T, int RQ_MAXCH>
 __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
+    if (A.doff[f + 1] - A.doff[f] <= A.wm_max) return;       /* done by k_rollq_wm */
     extern __shared__ __align__(16) unsigned char smem[];
     const int cap = A.cap;
     /* LDS carve-up (rollq_lds_bytes); single sorted buffer A: a merge reads the

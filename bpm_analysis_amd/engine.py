@@ -138,7 +138,7 @@ class Detector:
 
     def run(self, pcm, frame_offsets: Sequence[int], fs: int, params: dict, mode: str = "reference",
             stages: int = N.STAGE_ALL, channels: int = 1, out: Optional[Result] = None, want_y: bool = False,
-            d: Optional[Design] = None, log: bool = False) -> Result:
+            d: Optional[Design] = None, log: bool = False, options: int = 0) -> Result:
         """Run `stages` over a device batch.  `pcm` is a CUDA tensor (or None when
         ENVELOPE is not requested and `out.env` already holds the envelopes)."""
         if d is None:
@@ -155,6 +155,7 @@ class Detector:
         else:
             dt, pcm_ptr = N.DT_I16, None
         p = make_params(d, params, MODES[mode], stages, dt, channels)
+        p.options = options
         b = N.Batch()
         b.n_files = len(fo) - 1
         b.pcm = pcm_ptr
@@ -197,7 +198,8 @@ class Detector:
 
     # ------------------------------------------------------------------ #
     def run_host(self, recordings: List[np.ndarray], fs: int, params: dict, mode: str = "reference",
-                 stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False) -> List[dict]:
+                 stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False,
+                 options: int = 0) -> List[dict]:
         """Host arrays in, per-file host results out (H2D + run + D2H)."""
         torch = _torch()
         if not recordings:
@@ -211,12 +213,13 @@ class Detector:
         fo[1:] = np.cumsum([r.shape[0] for r in recordings])
         host = np.concatenate([np.ascontiguousarray(r).reshape(-1) for r in recordings])
         pcm = torch.from_numpy(host).to(self.device)
-        res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log)
+        res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log,
+                       options=options)
         torch.cuda.synchronize(self.device)
         return res.to_host()
 
     def run_env_host(self, envs: List[np.ndarray], sr: int, params: dict, stages: int,
-                     floors: Optional[List[np.ndarray]] = None) -> List[dict]:
+                     floors: Optional[List[np.ndarray]] = None, options: int = 0) -> List[dict]:
         """Detection stages on host envelopes (drop-in for the env-level functions)."""
         torch = _torch()
         fo = np.zeros(len(envs) + 1, dtype=np.int64)
@@ -226,7 +229,7 @@ class Detector:
         out.env.copy_(torch.from_numpy(np.concatenate(envs).astype(np.float64)).to(self.device))
         if floors is not None:
             out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
-        self.run(None, fo, d.sr, params, stages=stages, out=out, d=d)
+        self.run(None, fo, d.sr, params, stages=stages, out=out, d=d, options=options)
         torch.cuda.synchronize(self.device)
         return out.to_host()
 

@@ -69,6 +69,11 @@ enum bpmx_file_flag {
     BPMX_F_TOO_SHORT = 8     /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
 };
 
+enum bpmx_option {
+    BPMX_OPT_ROLLQ_MERGE = 1 /* force the sorted-union rolling quantile (test/diagnostic; default picks the
+                                wavelet-matrix kernel for recordings of <= 20480 decimated samples) */
+};
+
 typedef struct bpmx_ctx bpmx_ctx;
 
 typedef struct {
@@ -83,7 +88,7 @@ typedef struct {
     int32_t distance;      /* int(min_peak_distance_sec * sr) (:1066, :226), >= 1 */
     int32_t noise_window;  /* int(noise_window_sec * sr) (:1084) */
     int32_t min_periods;   /* 3 (:1085, :1105) */
-    int32_t reserved;
+    int32_t options;       /* bpmx_option bits (0 = defaults) */
     double trough_prom_q;  /* trough_prominence_quantile (:1067) */
     double peak_prom_q;    /* peak_prominence_quantile (:225) */
     double noise_floor_q;  /* noise_floor_quantile (:1075, :1085) */

@@ -191,3 +191,14 @@ def test_reference_side_ctypes_stub():
     assert sr == int(g["sr"])
     assert _same(env, g["env"]) and _same(floor, g["floor"])
     assert _same(tr, g["troughs"]) and _same(pk, g["peaks"])
+
+
+@pytest.mark.parametrize("name", ["ref_44k_60s_mono", "ref_44k_40s_clicks", "ref_96k_20s_stereo"])
+def test_rolling_quantile_kernels_agree(det, name):
+    """The wavelet-matrix rolling quantile (default) and the sorted-union kernel
+    (BPMX_OPT_ROLLQ_MERGE) both reproduce the golden floor bit for bit."""
+    from bpm_analysis_amd import _native as N
+    g = G.load(name)
+    for opt in (0, N.OPT_ROLLQ_MERGE):
+        r = det.run_host([g["pcm"]], int(g["fs"]), g["params"], mode="reference", options=opt)[0]
+        _check_file(r, g)

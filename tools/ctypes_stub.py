@@ -26,7 +26,7 @@ DT = {np.dtype(np.uint8): 0, np.dtype(np.int16): 1, np.dtype(np.int32): 2, np.dt
 class Params(ctypes.Structure):          # bpmx_params
     _fields_ = [(k, ctypes.c_int32) for k in ("mode", "stages", "dtype", "channels", "fs", "ds", "sr",
                                               "env_window", "distance", "noise_window", "min_periods",
-                                              "reserved")] + \
+                                              "options")] + \
                [(k, ctypes.c_double) for k in ("trough_prom_q", "peak_prom_q", "noise_floor_q", "fallback_q",
                                                "reject_mult")] + \
                [("ba_b", ctypes.c_double * 5), ("ba_a", ctypes.c_double * 5), ("ba_zi", ctypes.c_double * 4),

@@ -7,6 +7,7 @@
  */
 #define BPMX_STAMPS 1
 #include "../bpm_analysis_amd/csrc/k_floor.hip"
+#include "../bpm_analysis_amd/csrc/k_rollq_wm.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -92,6 +93,42 @@ int main(int argc, char **argv) {
         double tot = 0;
         for (int k = 0; k < 8; ++k) tot += sum[k];
         printf("T=%d cap=%d lds=%zu: %.3f ms; per-WG cycles (memtime) total %.0f\n", T, cap, lds, best, tot / F);
+        for (int k = 0; k < 8; ++k)
+            if (sum[k] > 0) printf("   %-10s %12.0f  %5.1f%%\n", names[k], sum[k] / F, 100.0 * sum[k] / tot);
+    }
+    {   /* wavelet-matrix kernel */
+        RollqArgs a;
+        a.dense = d_dense; a.doff = d_doff; a.troughs = d_tr; a.run = d_run; a.n_files = F; a.window = W;
+        a.min_periods = 3; a.cap = 0; a.q = 0.2; a.out = d_out; a.allnan = d_an; a.stamps = d_st; a.wm_max = WM_MMAX;
+        double *d_sorted;
+        CK(hipMalloc(&d_sorted, dense.size() * 8));
+
+        CK(hipMemset(d_st, 0, (size_t)F * 8 * 8));
+        const size_t lds = wm_lds_bytes(nd);
+        CK(hipFuncSetAttribute((const void *)k_rollq_wm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        float best = 1e9;
+        for (int rep = 0; rep < 4; ++rep) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(k_rollq_wm, dim3(F), dim3(WM_T), lds, 0, a, d_sorted);
+            CK(hipGetLastError());
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+        }
+        std::vector<unsigned long long> st((size_t)F * 8);
+        CK(hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost));
+        double sum[8] = {0};
+        for (int f = 0; f < F; ++f)
+            for (int k = 0; k < 8; ++k) sum[k] += (double)st[(size_t)f * 8 + k];
+        const char *names[8] = {"load", "count", "scan", "exchange", "sorted-out", "build", "query", "-"};
+        double tot = 0;
+        for (int k = 0; k < 8; ++k) tot += sum[k];
+        printf("k_rollq_wm lds=%zu: %.3f ms (4 reps best); per-WG cycles total %.0f\n", lds, best, tot / F);
         for (int k = 0; k < 8; ++k)
             if (sum[k] > 0) printf("   %-10s %12.0f  %5.1f%%\n", names[k], sum[k] / F, 100.0 * sum[k] / tot);
     }
