@@ -56,12 +56,14 @@ def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, 
         "k_find_peaks[peaks]": F * nd * 16,                # env + floor
         "k_interp": F * nd * 8,                            # dense written once
         "k_rolling_quantile": F * nd * 16,                 # dense in, quantile out
+        "k_rollq_wm": F * nd * 16,
         "k_sanitize": 0, "k_floor_final": F * nd * 8,
     }
     if mode == "native":
         return dict(common, **{
             "k_native_blocks": F * n_frames * channels * 2,      # every PCM sample read once
-            "k_native_scan": F * (nb * (64 + 32 + 32) + nd * (8 + 2 * channels)),
+            "k_native_carry": F * (nb // 64 * 128 + 64 * 16 * 8),  # tile carries in/out, partial tile
+            "k_native_yd": F * nb * (8 + 8),                          # gamma in, yd out
             "rocfft_r2c": F * (nd * 8 + half * 16),
             "k_hilbert_weights": F * half * 16 * 2,
             "rocfft_c2c_inv": F * nd * 16 * 2,

@@ -30,8 +30,8 @@ struct bpmx_ctx {
     /* native-mode block-state tables (host copies back the async uploads) */
     std::vector<int64_t> nat_key;
     std::vector<double> nat_tab;
-    std::vector<int64_t> nat_boff;
-    std::vector<int64_t> nat_tkey, nat_tdoff;   /* tile-list geometry key */
+    std::vector<int64_t> nat_boff;              /* block offsets | per-file tile offsets */
+    std::vector<int64_t> nat_tkey;              /* tile-list geometry key */
     std::vector<char> nat_tiles;                /* host copy of the tile list */
     bool nat_tiles_dirty = false;
     bool nat_tab_dirty = false;

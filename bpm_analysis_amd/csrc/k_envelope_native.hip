@@ -5,21 +5,22 @@
  * oracle: scipy/signal/_signaltools.py:4718-4829 (sosfiltfilt), :2318 (hilbert),
  * composed as SURVEY.md §8(a) A13 defines; tolerance 1e-9 relative on env.
  *
- * sosfiltfilt is linear and time-invariant, so the per-sample recursion over
- * one decimation block of ds samples collapses to 8 dot products (the block's
- * forward-state increment u_j and backward-state increment v_j; tables from
- * bpm_analysis_amd/native_tables.py).  That turns the HBM-bound part into a
- * fully parallel, coalesced streaming kernel:
+ * sosfiltfilt is linear and time-invariant, so over one decimation block of
+ * ds samples the per-sample recursion collapses to 8 dot products (the
+ * block's forward-state increment u_j and backward-state increment v_j), and
+ * over a tile of T blocks the two block recursions collapse again to tile
+ * carries (bpm_analysis_amd/native_tables.py: tables, model_tiled):
  *
- *   k_native_blocks  every PCM sample read once from HBM (a tile of 128
- *                    blocks staged in LDS), 8 f64 FMA per sample,
- *                    64 B of (u_j, v_j) written per block.
- *   k_native_scan    one wave per recording: affine scans over blocks (lane
- *                    segments + a Kogge-Stone combine of 4x4 affine maps) for
- *                    the forward states S_j and backward states Q_j, the exact
- *                    per-sample recursion over the 15-sample head pad and the
- *                    <= ds+15-sample tail, and the decimated output
- *                    yd_j = C Q_j + D (C S_j + D x[j*ds]).
+ *   k_native_blocks  every PCM sample read once from HBM (coalesced tile
+ *                    loads, LDS staging), 8 f64 FMA per sample; then, per
+ *                    tile, two Kogge-Stone scans over the 64 lanes (forward
+ *                    local states, backward suffix sums) leave ONE f64 per
+ *                    block (gamma_j) and 64 B per tile of carry inputs.
+ *   k_native_carry   one wave per recording: the 15-sample head pad, the
+ *                    tile-to-tile carries S0_t (forward) and Qe_t (backward),
+ *                    the partial last tile and the <= ds+15-sample tail by
+ *                    exact recursion.
+ *   k_native_yd      yd_j = alpha_b . Qe_t + beta_b . S0_t + gamma_j.
  *   rocFFT           R2C + C2C inverse (Hilbert), one plan per (Nd, batch).
  *   k_hilbert_weights  the analytic-signal weights h (1, 2, ..., 1, 0, ...).
  *   k_native_env     |z|/Nd and the centred rolling mean, LDS-tiled.
@@ -41,30 +42,46 @@ namespace bpmx {
 /* table layout (native_tables.pack) */
 enum { TB_A = 0, TB_B = 16, TB_C = 20, TB_D = 24, TB_M = 25, TB_P = 41, TB_ZI = 57, TB_COEF = 64 };
 
-struct NatTile;
-struct NatBlockArgs {
-    const void *pcm;
-    const int64_t *foff, *boff;   /* frame offsets, block offsets (blocks = Nd-1 per file) */
-    const int64_t *boffp;         /* padded per-file block storage: 64 * ceil(nb/64) entries */
-    const struct NatTile *tiles;  /* int16 mono path: tile list */
-    int64_t n_tiles, total;       /* tiles; samples in pcm */
-    int bt;                       /* blocks per tile */
-    const int32_t *active;
-    int32_t n_files, channels, ds;
-    const double *tab;
-    double *uv;                    /* [sum blocks][8] */
+/* tile tables, after the coefficient rows (native_tables.tile_tables) */
+enum { TT_KPOW = 0, TT_MT = 96, TT_G0 = 112, TT_ALPHA = 128, TT_BETA = 384, TT_SIZE = 640 };
+constexpr int NAT_PART = 16;          /* doubles per partial-tile block record: u4 v4 x pad3 S4 */
+
+struct NatTile {
+    int64_t s0;                         /* first frame of the tile (index into pcm frames) */
+    int64_t gbase;                      /* boff[f] + j0: gamma index of the tile's first block */
+    int64_t ybase;                      /* doff[f] + j0: yd index of the tile's first block */
+    int32_t j0, nb;                     /* first block, blocks of the file */
+    int32_t f, pad;
 };
 
-struct NatScanArgs {
+struct NatBlockArgs {
     const void *pcm;
-    const int64_t *foff, *doff, *boff, *boffp;
+    const NatTile *tiles;
+    int64_t n_tiles, total;       /* tiles; samples in pcm (int16 path) */
+    int32_t bt, channels, ds;     /* blocks per (full) tile */
+    const double *tab, *tt;       /* block tables; tile tables */
+    double *gam;                  /* [sum blocks] */
+    double *agg;                  /* [n_tiles][8]: forward tile sum, backward R_0 */
+    double *part;                 /* [F][64][NAT_PART]: raw blocks of each file's partial last tile */
+};
+
+struct NatCarryArgs {
+    const void *pcm;
+    const int64_t *foff, *doff, *boff, *toff;
     const int32_t *active;
-    int32_t n_files, dtype, channels, ds;
-    const double *tab;
-    const double *uv;
-    double *S;                     /* [sum blocks][4] forward block-start states */
+    int32_t n_files, dtype, channels, ds, bt;
+    const double *tab, *tt, *agg;
+    double *part;                  /* partial-tile blocks; k_native_carry adds their states */
+    double *carry;                 /* [n_tiles][8]: S0_t, Qe_t */
     double *tail;                  /* [F][ds+16] */
-    double *yd;                    /* [sumNd] decimated filtered signal */
+    double *yd;
+};
+
+struct NatYdArgs {
+    const NatTile *tiles;
+    int32_t bt;
+    const double *tt, *carry, *gam;
+    double *yd;
 };
 
 struct NatEnvArgs {
@@ -76,161 +93,6 @@ struct NatEnvArgs {
 };
 
 /* ---------------------------------------------------------------------- */
-/* k_native_blocks: per decimation block j of every file
- *   u_j = sum_{i<ds} F_i x[j*ds+i],  v_j = sum_{i<=ds} G_i x[j*ds+i]          */
-
-template <int DT, bool MULTI>
-__device__ __forceinline__ double nat_frame(const void *__restrict__ pcm, int ch, int64_t frame) {
-    if (!MULTI) {
-        switch (DT) {
-        case BPMX_DT_U8: return (double)((const uint8_t *)pcm)[frame];
-        case BPMX_DT_I16: return (double)((const int16_t *)pcm)[frame];
-        case BPMX_DT_I32: return (double)((const int32_t *)pcm)[frame];
-        case BPMX_DT_F32: return (double)((const float *)pcm)[frame];
-        default: return ((const double *)pcm)[frame];
-        }
-    }
-    return frame_value(pcm, DT, ch, frame);
-}
-
-/* int16 mono fast path.  Persistent single-wave workgroups walk a list of
- * tiles (up to 64 consecutive blocks of one file).  A tile's samples arrive
- * with coalesced 16-byte loads into registers — issued one tile AHEAD, so
- * HBM latency hides behind the current tile's FMAs — then go through LDS,
- * where lane b reads block b's ds+1 samples (lane stride ds/2 dwords: odd for
- * the usual ds, conflict-free).  The 8 coefficients of each sample are
- * wave-uniform scalar loads. */
-constexpr int NB_RCH = 20;              /* 16-byte chunks per lane per tile: <= 10240 samples */
-struct NatTile {
-    int64_t s0;                         /* first sample of the tile (index into pcm) */
-    int64_t ebase;                      /* boffp[f] */
-    int32_t j0, nb;                     /* first block, blocks of the file */
-};
-
-__device__ __forceinline__ double nat_lo16(uint32_t w) { return (double)(int)(int16_t)(w & 0xFFFFu); }
-__device__ __forceinline__ double nat_hi16(uint32_t w) { return (double)((int)w >> 16); }
-
-typedef uint32_t nat_u4 __attribute__((ext_vector_type(4)));
-/* `coef` is passed separately as __restrict__ so its loads become scalar
- * (wave-uniform) loads: the compiler must know the uv stores cannot alias it */
-__global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const double *__restrict__ coef) {
-    typedef nat_u4 u4;
-    __shared__ u4 tile[NB_RCH * 64];
-    const int lane = threadIdx.x;
-    const int16_t *pcm = (const int16_t *)A.pcm;
-    const int64_t total = A.total;
-    const int ds = A.ds, bt = A.bt;
-    const int nch = (7 + bt * ds + 1 + 7) >> 3;           /* chunks a tile may touch */
-    auto issue = [&](int64_t t, u4 *reg, int &off) {
-        const int64_t s0 = A.tiles[t].s0;
-        const int64_t a0 = s0 & ~(int64_t)7;
-        off = (int)(s0 - a0);
-#pragma unroll
-        for (int r = 0; r < NB_RCH; ++r) {
-            const int q = r * 64 + lane;
-            const int64_t c = a0 + (int64_t)q * 8;
-            if (q < nch && c + 8 <= total) __builtin_memcpy(&reg[r], pcm + c, 16);
-            else reg[r] = u4{0, 0, 0, 0};      /* a partial last chunk is patched in LDS */
-        }
-    };
-    u4 reg[NB_RCH];
-    int off = 0;
-    int64_t t = blockIdx.x;
-    if (t < A.n_tiles) issue(t, reg, off);
-    while (t < A.n_tiles) {
-        const NatTile tl = A.tiles[t];
-#pragma unroll
-        for (int r = 0; r < NB_RCH; ++r) tile[r * 64 + lane] = reg[r];
-        const int coff = off;
-        {
-            const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
-            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))
-                ((int16_t *)tile)[tail0 - a0 + lane] = pcm[tail0 + lane];
-        }
-        __syncthreads();
-        const int64_t tn = t + gridDim.x;
-        if (tn < A.n_tiles) issue(tn, reg, off);
-        const int j = tl.j0 + lane;
-        if (lane < bt && j < tl.nb) {
-            const int base = coff + lane * ds;                        /* halfword index in the tile */
-            const uint32_t *wp = (const uint32_t *)tile + (base >> 1);
-            const uint32_t sh = (base & 1) ? 16u : 0u;
-            double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-            auto acc = [&](double xv, const double *c) {
-                u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
-                u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
-                v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
-                v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
-            };
-            const int L = ds + 1;                                    /* row ds has F = 0 */
-            int i = 0;
-            for (; i + 8 <= L; i += 8) {
-                const uint32_t *p = wp + i / 2;
-                const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
-                const uint32_t d0 = __builtin_amdgcn_alignbit(w1, w0, sh);
-                const uint32_t d1 = __builtin_amdgcn_alignbit(w2, w1, sh);
-                const uint32_t d2 = __builtin_amdgcn_alignbit(w3, w2, sh);
-                const uint32_t d3 = __builtin_amdgcn_alignbit(w4, w3, sh);
-                const double *cr = coef + (int64_t)i * 8;
-                acc(nat_lo16(d0), cr + 0);  acc(nat_hi16(d0), cr + 8);
-                acc(nat_lo16(d1), cr + 16); acc(nat_hi16(d1), cr + 24);
-                acc(nat_lo16(d2), cr + 32); acc(nat_hi16(d2), cr + 40);
-                acc(nat_lo16(d3), cr + 48); acc(nat_hi16(d3), cr + 56);
-            }
-            const int16_t *th = (const int16_t *)tile;
-            for (; i < L; ++i) acc((double)th[base + i], coef + (int64_t)i * 8);
-            const uint32_t R = ((uint32_t)tl.nb + 63u) >> 6;
-            const int64_t e = tl.ebase + (int64_t)((uint32_t)j % R) * 64 + (uint32_t)j / R;
-            double2 *o = (double2 *)(A.uv + e * 8);
-            o[0] = make_double2(u0, u1); o[1] = make_double2(u2, u3);
-            o[2] = make_double2(v0, v1); o[3] = make_double2(v2, v3);
-        }
-        __syncthreads();
-        t = tn;
-    }
-}
-
-/* generic path (other sample formats, multi-channel): f64 tile, 32 blocks per group */
-template <int DT, bool MULTI>
-__global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
-    constexpr int NBG = 32;
-    extern __shared__ __align__(16) double tile_d[];   /* 32*ds + 1 */
-    double *tile = tile_d;
-    const int f = blockIdx.y;
-    if (f >= A.n_files || !A.active[f]) return;
-    const int64_t nb = A.boff[f + 1] - A.boff[f];
-    const int64_t j0 = (int64_t)blockIdx.x * NBG;
-    if (j0 >= nb) return;
-    const int ds = A.ds, tid = threadIdx.x;
-    const int64_t nblk = nb - j0 < NBG ? nb - j0 : NBG;
-    const int64_t nsamp = nblk * ds + 1;
-    const int64_t fb = A.foff[f] + j0 * ds;
-    for (int64_t i = tid; i < nsamp; i += 64) tile[i] = nat_frame<DT, MULTI>(A.pcm, A.channels, fb + i);
-    __syncthreads();
-    if (tid >= nblk) return;
-    const double *__restrict__ coef = A.tab + TB_COEF;
-    const double *x = tile + tid * ds;
-    double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-    for (int i = 0; i < ds; ++i) {
-        const double xv = x[i];
-        const double *c = coef + i * 8;
-        u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
-        u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
-        v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
-        v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
-    }
-    {
-        const double xv = x[ds];
-        const double *c = coef + ds * 8;
-        v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
-        v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
-    }
-    const int64_t j = j0 + tid, R = (nb + 63) >> 6;
-    double2 *o = (double2 *)(A.uv + (A.boffp[f] + (j % R) * 64 + j / R) * 8);
-    o[0] = make_double2(u0, u1); o[1] = make_double2(u2, u3);
-    o[2] = make_double2(v0, v1); o[3] = make_double2(v2, v3);
-}
-
 /* ---------------------------------------------------------------------- */
 /* 4x4 affine-map helpers (row-major matrices in registers) */
 struct V4 { double a, b, c, d; };
@@ -308,143 +170,286 @@ struct SosStep {
     }
 };
 
-/* One wave per recording.  Block j of the file is held by lane j / R at step
- * t = j % R (R = ceil(nb/64)); per-block data lives at [t][lane], so each step
- * of the lane loops is one coalesced 4-KiB access, prefetched one step ahead. */
-__global__ __launch_bounds__(64) void k_native_scan(NatScanArgs A, SosStep SS) {
-    const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f]) return;
+/* k_native_blocks: per decimation block j of every file
+ *   u_j = sum_{i<ds} F_i x[j*ds+i],  v_j = sum_{i<=ds} G_i x[j*ds+i]          */
+
+template <int DT, bool MULTI>
+__device__ __forceinline__ double nat_frame(const void *__restrict__ pcm, int ch, int64_t frame) {
+    if (!MULTI) {
+        switch (DT) {
+        case BPMX_DT_U8: return (double)((const uint8_t *)pcm)[frame];
+        case BPMX_DT_I16: return (double)((const int16_t *)pcm)[frame];
+        case BPMX_DT_I32: return (double)((const int32_t *)pcm)[frame];
+        case BPMX_DT_F32: return (double)((const float *)pcm)[frame];
+        default: return ((const double *)pcm)[frame];
+        }
+    }
+    return frame_value(pcm, DT, ch, frame);
+}
+
+/* Per-tile epilogue shared by the block kernels (all 64 lanes call it; lane b
+ * holds block j0+b's u, v and first sample x).  A full tile (bt blocks) is
+ * reduced to gamma_b = C R_b + D C loc_b + D^2 x_b per block plus its carry
+ * inputs (forward tile sum, backward R_0); the file's partial last tile keeps
+ * its raw blocks for k_native_carry's exact recursion. */
+__device__ __forceinline__ V4 nat_ld4(const double *p) { return V4{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ M4 nat_ld16(const double *p) {
+    M4 r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r.m[i] = p[i];
+    return r;
+}
+__device__ __forceinline__ double dot4(const V4 &a, const V4 &b) {
+    return __builtin_fma(a.a, b.a, __builtin_fma(a.b, b.b, __builtin_fma(a.c, b.c, a.d * b.d)));
+}
+
+__device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const NatTile &tl, int64_t t, int lane,
+                                                  bool valid, V4 u, V4 v, double x) {
+    const int bt = A.bt;
+    const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
+    if (Lt < bt) {                                        /* partial last tile: raw blocks */
+        if (valid) {
+            double *pp = A.part + ((int64_t)tl.f * 64 + lane) * NAT_PART;
+            pp[0] = u.a; pp[1] = u.b; pp[2] = u.c; pp[3] = u.d;
+            pp[4] = v.a; pp[5] = v.b; pp[6] = v.c; pp[7] = v.d;
+            pp[8] = x;
+        }
+        return;
+    }
+    const double *__restrict__ tb = A.tab;
+    const double *__restrict__ tt = A.tt;
+    if (!valid) { u = V4{0, 0, 0, 0}; v = V4{0, 0, 0, 0}; x = 0; }
+    /* incl_b = sum_{c<=b} M^(b-c) u_c */
+    V4 incl = u;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int d = 1 << k;
+        const V4 y = shfl_up_v(incl, d);
+        if (lane >= d) incl = add4(incl, mv(nat_ld16(tt + TT_KPOW + 16 * k), y));
+    }
+    V4 loc = shfl_up_v(incl, 1);
+    if (lane == 0) loc = V4{0, 0, 0, 0};
+    /* R_b = sum_{c>=b} M^(c-b) (P loc_c + v_c) */
+    V4 R = valid ? add4(mv(nat_ld16(tb + TB_P), loc), v) : V4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int d = 1 << k;
+        const V4 y = shfl_down_v(R, d);
+        if (lane + d < 64) R = add4(R, mv(nat_ld16(tt + TT_KPOW + 16 * k), y));
+    }
+    const V4 C = nat_ld4(tb + TB_C);
+    const double D = tb[TB_D];
+    if (valid) A.gam[tl.gbase + lane] = dot4(C, R) + D * dot4(C, loc) + D * D * x;
+    double *ag = A.agg + t * 8;
+    if (lane == bt - 1) { ag[0] = incl.a; ag[1] = incl.b; ag[2] = incl.c; ag[3] = incl.d; }
+    if (lane == 0) { ag[4] = R.a; ag[5] = R.b; ag[6] = R.c; ag[7] = R.d; }
+}
+
+/* int16 mono fast path.  Persistent single-wave workgroups walk the tile
+ * list (bt consecutive blocks of one file per tile).  A tile's samples arrive
+ * with coalesced 16-byte loads into registers — issued one tile AHEAD, so
+ * HBM latency hides behind the current tile's FMAs — then go through LDS,
+ * where lane b reads block b's ds+1 samples (lane stride ds/2 dwords: odd for
+ * the usual ds, conflict-free).  The 8 coefficients of each sample are
+ * wave-uniform scalar loads. */
+constexpr int NB_RCH = 20;              /* 16-byte chunks per lane per tile: <= 10240 samples */
+
+__device__ __forceinline__ double nat_lo16(uint32_t w) { return (double)(int)(int16_t)(w & 0xFFFFu); }
+__device__ __forceinline__ double nat_hi16(uint32_t w) { return (double)((int)w >> 16); }
+
+typedef uint32_t nat_u4 __attribute__((ext_vector_type(4)));
+
+/* `coef` is passed separately as __restrict__ so its loads become scalar
+ * (wave-uniform) loads: the compiler must know the stores cannot alias it */
+__global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const double *__restrict__ coef) {
+    typedef nat_u4 u4;
+    __shared__ u4 tile[NB_RCH * 64];
     const int lane = threadIdx.x;
+    const int16_t *pcm = (const int16_t *)A.pcm;
+    const int64_t total = A.total;
+    const int ds = A.ds, bt = A.bt;
+    const int nch = (7 + bt * ds + 1 + 7) >> 3;           /* chunks a tile may touch */
+    auto issue = [&](int64_t t, u4 *reg, int &off) {
+        const int64_t s0 = A.tiles[t].s0;
+        const int64_t a0 = s0 & ~(int64_t)7;
+        off = (int)(s0 - a0);
+#pragma unroll
+        for (int r = 0; r < NB_RCH; ++r) {
+            const int q = r * 64 + lane;
+            const int64_t c = a0 + (int64_t)q * 8;
+            if (q < nch && c + 8 <= total) __builtin_memcpy(&reg[r], pcm + c, 16);
+            else reg[r] = u4{0, 0, 0, 0};      /* a partial last chunk is patched in LDS */
+        }
+    };
+    u4 reg[NB_RCH];
+    int off = 0;
+    int64_t t = blockIdx.x;
+    if (t < A.n_tiles) issue(t, reg, off);
+    while (t < A.n_tiles) {
+        const NatTile tl = A.tiles[t];
+#pragma unroll
+        for (int r = 0; r < NB_RCH; ++r) tile[r * 64 + lane] = reg[r];
+        const int coff = off;
+        {
+            const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
+            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))
+                ((int16_t *)tile)[tail0 - a0 + lane] = pcm[tail0 + lane];
+        }
+        __syncthreads();
+        const int64_t tn = t + gridDim.x;
+        if (tn < A.n_tiles) issue(tn, reg, off);
+        const int j = tl.j0 + lane;
+        const bool valid = lane < bt && j < tl.nb;
+        double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0, x0 = 0;
+        if (valid) {
+            const int base = coff + lane * ds;                        /* halfword index in the tile */
+            const uint32_t *wp = (const uint32_t *)tile + (base >> 1);
+            const uint32_t sh = (base & 1) ? 16u : 0u;
+            auto acc = [&](double xv, const double *c) {
+                u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
+                u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
+                v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
+                v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
+            };
+            const int L = ds + 1;                                    /* row ds has F = 0 */
+            int i = 0;
+            for (; i + 8 <= L; i += 8) {
+                const uint32_t *p = wp + i / 2;
+                const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+                const uint32_t d0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+                const uint32_t d1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+                const uint32_t d2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+                const uint32_t d3 = __builtin_amdgcn_alignbit(w4, w3, sh);
+                const double *cr = coef + (int64_t)i * 8;
+                acc(nat_lo16(d0), cr + 0);  acc(nat_hi16(d0), cr + 8);
+                acc(nat_lo16(d1), cr + 16); acc(nat_hi16(d1), cr + 24);
+                acc(nat_lo16(d2), cr + 32); acc(nat_hi16(d2), cr + 40);
+                acc(nat_lo16(d3), cr + 48); acc(nat_hi16(d3), cr + 56);
+            }
+            const int16_t *th = (const int16_t *)tile;
+            for (; i < L; ++i) acc((double)th[base + i], coef + (int64_t)i * 8);
+            x0 = (double)th[base];
+        }
+        nat_tile_epilogue(A, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+        __syncthreads();
+        t = tn;
+    }
+}
+
+/* generic path (other sample formats, multi-channel): one wave per tile, each
+ * lane reads its block straight from global memory */
+template <int DT, bool MULTI>
+__global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
+    const int64_t t = blockIdx.x;
+    if (t >= A.n_tiles) return;
+    const NatTile tl = A.tiles[t];
+    const int lane = threadIdx.x, ds = A.ds;
+    const int j = tl.j0 + lane;
+    const bool valid = lane < A.bt && j < tl.nb;
+    double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0, x0 = 0;
+    if (valid) {
+        const double *__restrict__ coef = A.tab + TB_COEF;
+        const int64_t fb = tl.s0 + (int64_t)lane * ds;
+        for (int i = 0; i <= ds; ++i) {
+            const double xv = nat_frame<DT, MULTI>(A.pcm, A.channels, fb + i);
+            const double *c = coef + i * 8;                      /* row ds has F = 0 */
+            u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
+            u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
+            v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
+            v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
+            if (i == 0) x0 = xv;
+        }
+    }
+    nat_tile_epilogue(A, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+}
+
+/* One wave per recording (lane 0 carries the sequential recursions):
+ *   head  15 padded samples, exact sosfilt steps -> S at block 0;
+ *   tiles S0_(t+1) = M^T S0_t + incl_t (forward carries, stored per tile);
+ *   partial last tile: exact block recursion forward, then backward with
+ *         its decimated outputs;
+ *   tail  [c_(nd-1), ne): exact forward then backward per-sample recursion
+ *         -> Q at block nb and yd[nd-1];
+ *   tiles Qe_t stored, Q_start = M^T Qe_t + R0_t + G0 S0_t (backward). */
+__global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files || !A.active[f] || threadIdx.x != 0) return;
     const int64_t nd = A.doff[f + 1] - A.doff[f];
     const int64_t nb = nd - 1;
     const int64_t n = A.foff[f + 1] - A.foff[f];
     const int64_t fb = A.foff[f];
-    const int ds = A.ds;
+    const int ds = A.ds, bt = A.bt;
     const int wdt = work_dtype(A.dtype, A.channels);
-    const double *tb = A.tab;
-    M4 Mm, Pm;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { Mm.m[i] = tb[TB_M + i]; Pm.m[i] = tb[TB_P + i]; }
-    const V4 Cv{tb[TB_C], tb[TB_C + 1], tb[TB_C + 2], tb[TB_C + 3]};
+    const double *tb = A.tab, *tt = A.tt;
+    const M4 Mm = nat_ld16(tb + TB_M), Pm = nat_ld16(tb + TB_P), MT = nat_ld16(tt + TT_MT), G0 = nat_ld16(tt + TT_G0);
+    const V4 Cv = nat_ld4(tb + TB_C);
     const double Dd = tb[TB_D];
-    const V4 zi{tb[TB_ZI], tb[TB_ZI + 1], tb[TB_ZI + 2], tb[TB_ZI + 3]};
+    const V4 zi = nat_ld4(tb + TB_ZI);
     auto x = [&](int64_t k) { return frame_value(A.pcm, A.dtype, A.channels, fb + k); };
-    const double4 *uv = (const double4 *)(A.uv + A.boffp[f] * 8);   /* entry e: uv[2e] = u, uv[2e+1] = v */
-    double4 *S = (double4 *)(A.S + A.boffp[f] * 4);
     double *yd = A.yd + A.doff[f];
 
-    /* (a) head: 15 padded samples, exact recursion (redundant in every lane) */
-    V4 s0;
+    V4 S;
     {
         const double x0 = x(0);
         const double e0 = odd_ext(wdt, x0, x(15));
         V4 z{zi.a * e0, zi.b * e0, zi.c * e0, zi.d * e0};
         for (int k = 0; k < 15; ++k) (void)SS.step(z, odd_ext(wdt, x0, x(15 - k)));
-        s0 = z;
+        S = z;
     }
-    const int64_t R = (nb + 63) >> 6;
-    const int64_t lo = lane * R < nb ? lane * R : nb;
-    const int64_t len = (lo + R < nb ? lo + R : nb) - lo;
-    auto U = [&](int64_t t) { const double4 w = uv[2 * (t * 64 + lane)]; return V4{w.x, w.y, w.z, w.w}; };
-    auto Vv = [&](int64_t t) { const double4 w = uv[2 * (t * 64 + lane) + 1]; return V4{w.x, w.y, w.z, w.w}; };
-
-    /* (b) forward: segment map a = sum M^.. u, then Kogge-Stone across lanes */
-    V4 a{0, 0, 0, 0};
+    const int64_t t0 = A.toff[f];
+    const int64_t Tf = nb / bt;                             /* full tiles */
+    const int Lp = (int)(nb - Tf * bt);                     /* blocks in the partial tile */
+    for (int64_t t = t0; t < t0 + Tf; ++t) {
+        double *c = A.carry + t * 8;
+        c[0] = S.a; c[1] = S.b; c[2] = S.c; c[3] = S.d;
+        S = add4(mv(MT, S), nat_ld4(A.agg + t * 8));
+    }
+    double *pp = A.part + (int64_t)f * 64 * NAT_PART;
+    for (int b = 0; b < Lp; ++b) {
+        double *r = pp + b * NAT_PART;
+        r[12] = S.a; r[13] = S.b; r[14] = S.c; r[15] = S.d;
+        S = add4(mv(Mm, S), nat_ld4(r));
+    }
+    /* tail [c_{nd-1}, ne): exact forward then backward recursion */
+    double *tl = A.tail + (int64_t)f * (ds + 16);
+    const int64_t base = (nd - 1) * ds;                     /* x index of c_{nd-1} */
+    const int64_t nt = n - base + 15;                       /* tail length incl. right pad */
+    const double xl = x(n - 1);
     {
-        V4 un = R > 0 ? U(0) : V4{0, 0, 0, 0};
-        for (int64_t t = 0; t < R; ++t) {
-            const V4 uc = un;
-            if (t + 1 < R) un = U(t + 1);
-            if (t < len) a = add4(mv(Mm, a), uc);
-        }
-    }
-    const M4 Tl = mpow(Mm, len);
-    M4 T = Tl;
-    for (int d = 1; d < 64; d <<= 1) {
-        const M4 To = shfl_up_m(T, d);
-        const V4 ao = shfl_up_v(a, d);
-        if (lane >= d) { a = add4(mv(T, ao), a); T = mm(T, To); }
-    }
-    M4 Te = shfl_up_m(T, 1);
-    V4 ae = shfl_up_v(a, 1);
-    if (lane == 0) { Te = eye4(); ae = V4{0, 0, 0, 0}; }
-    V4 st = add4(mv(Te, s0), ae);
-    {
-        V4 un = R > 0 ? U(0) : V4{0, 0, 0, 0};
-        for (int64_t t = 0; t < R; ++t) {
-            const V4 uc = un;
-            if (t + 1 < R) un = U(t + 1);
-            if (t < len) {
-                S[t * 64 + lane] = make_double4(st.a, st.b, st.c, st.d);
-                st = add4(mv(Mm, st), uc);
-            }
-        }
-    }
-    const int last_lane = nb > 0 ? (int)((nb - 1) / R) : 0;
-    V4 slast = shfl_v(st, last_lane);
-    if (nb == 0) slast = s0;
-
-    /* (c) tail [c_{nd-1}, ne): exact forward then backward recursion, lane 0 */
-    __shared__ double s_q[4];
-    if (lane == 0) {
-        double *tl = A.tail + (int64_t)f * (ds + 16);
-        const int64_t base = (nd - 1) * ds;     /* x index of c_{nd-1} */
-        const int64_t nt = n - base + 15;         /* tail length incl. right pad */
-        const double xl = x(n - 1);
-        V4 z = slast;
+        V4 z = S;
         for (int64_t k = 0; k < nt; ++k) {
             const int64_t xi = base + k;
             const double u = xi < n ? x(xi) : odd_ext(wdt, xl, x(n - 2 - (xi - n)));
             tl[k] = SS.step(z, u);
         }
-        const double y0 = tl[nt - 1];
-        V4 q{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
-        for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, tl[k]);
-        s_q[0] = q.a; s_q[1] = q.b; s_q[2] = q.c; s_q[3] = q.d;
-        yd[nd - 1] = Cv.a * q.a + Cv.b * q.b + Cv.c * q.c + Cv.d * q.d + Dd * tl[0];
     }
-    __syncthreads();
-    const V4 qlast{s_q[0], s_q[1], s_q[2], s_q[3]};
+    const double y0 = tl[nt - 1];
+    V4 q{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
+    for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, tl[k]);
+    yd[nd - 1] = dot4(Cv, q) + Dd * tl[0];
+    for (int b = Lp - 1; b >= 0; --b) {
+        const double *r = pp + b * NAT_PART;
+        const V4 Sj = nat_ld4(r + 12);
+        q = add4(mv(Mm, q), add4(mv(Pm, Sj), nat_ld4(r + 4)));
+        yd[Tf * bt + b] = dot4(Cv, q) + Dd * (dot4(Cv, Sj) + Dd * r[8]);
+    }
+    for (int64_t t = t0 + Tf - 1; t >= t0; --t) {
+        double *c = A.carry + t * 8;
+        c[4] = q.a; c[5] = q.b; c[6] = q.c; c[7] = q.d;
+        q = add4(add4(mv(MT, q), nat_ld4(A.agg + t * 8 + 4)), mv(G0, nat_ld4(c)));
+    }
+}
 
-    /* (d) backward: Q_j = M Q_{j+1} + P S_j + v_j from Q_{nb} = qlast */
-    auto Sv = [&](int64_t t) { const double4 w = S[t * 64 + lane]; return V4{w.x, w.y, w.z, w.w}; };
-    V4 b{0, 0, 0, 0};
-    {
-        V4 sn = R > 0 ? Sv(R - 1) : V4{0, 0, 0, 0}, vn = R > 0 ? Vv(R - 1) : V4{0, 0, 0, 0};
-        for (int64_t t = R - 1; t >= 0; --t) {
-            const V4 sc = sn, vc = vn;
-            if (t > 0) { sn = Sv(t - 1); vn = Vv(t - 1); }
-            if (t < len) b = add4(mv(Mm, b), add4(mv(Pm, sc), vc));
-        }
-    }
-    T = Tl;
-    for (int d = 1; d < 64; d <<= 1) {
-        const M4 To = shfl_down_m(T, d);
-        const V4 bo = shfl_down_v(b, d);
-        if (lane + d < 64) { b = add4(mv(T, bo), b); T = mm(T, To); }
-    }
-    Te = shfl_down_m(T, 1);
-    V4 be = shfl_down_v(b, 1);
-    if (lane == 63) { Te = eye4(); be = V4{0, 0, 0, 0}; }
-    V4 q = add4(mv(Te, qlast), be);
-    {
-        V4 sn = R > 0 ? Sv(R - 1) : V4{0, 0, 0, 0}, vn = R > 0 ? Vv(R - 1) : V4{0, 0, 0, 0};
-        double xn = len > 0 ? x((lo + (R - 1 < len - 1 ? R - 1 : len - 1)) * ds) : 0.0;
-        for (int64_t t = R - 1; t >= 0; --t) {
-            const V4 sc = sn, vc = vn;
-            const double xc = xn;
-            if (t > 0) {
-                sn = Sv(t - 1); vn = Vv(t - 1);
-                const int64_t tt = t - 1 < len - 1 ? t - 1 : (len > 0 ? len - 1 : 0);
-                xn = x((lo + tt) * ds);
-            }
-            if (t < len) {
-                q = add4(mv(Mm, q), add4(mv(Pm, sc), vc));
-                const double yf = Cv.a * sc.a + Cv.b * sc.b + Cv.c * sc.c + Cv.d * sc.d + Dd * xc;
-                yd[lo + t] = Cv.a * q.a + Cv.b * q.b + Cv.c * q.c + Cv.d * q.d + Dd * yf;
-            }
-        }
-    }
+/* yd_j = alpha_b . Qe_t + beta_b . S0_t + gamma_j over full tiles (lane = block) */
+__global__ __launch_bounds__(64) void k_native_yd(NatYdArgs A) {
+    const int64_t t = blockIdx.x;
+    const NatTile tl = A.tiles[t];
+    const int bt = A.bt, lane = threadIdx.x;
+    if (tl.nb - tl.j0 < bt || lane >= bt) return;          /* partial tiles: k_native_carry */
+    const double *c = A.carry + t * 8;
+    const V4 S0 = nat_ld4(c), Qe = nat_ld4(c + 4);
+    const V4 al = nat_ld4(A.tt + TT_ALPHA + 4 * lane), be = nat_ld4(A.tt + TT_BETA + 4 * lane);
+    A.yd[tl.ybase + lane] = dot4(al, Qe) + dot4(be, S0) + A.gam[tl.gbase + lane];
 }
 
 /* ---------------------------------------------------------------------- */
@@ -572,7 +577,7 @@ void lm_vec(const LM &X, const LD *v, LD *out) {
     }
 }
 
-std::vector<double> build_tables(const double *sos, const double *sos_zi, int L) {
+std::vector<double> build_tables(const double *sos, const double *sos_zi, int L, int T) {
     /* probe the cascade step: s' = A s + B u, y = C s + D u */
     auto step = [&](const LD *z, LD u, LD *zo) -> LD {
         const LD *a = nullptr; (void)a;
@@ -618,7 +623,7 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L)
         for (int r = 0; r < 4; ++r)
             for (int c = 0; c < 4; ++c) P.m[r * 4 + c] += AB[(size_t)(i - 1) * 4 + r] * CA[c];
     }
-    std::vector<double> out(64 + 8 * (size_t)(L + 1), 0.0);
+    std::vector<double> out(64 + 8 * (size_t)(L + 1) + TT_SIZE, 0.0);
     for (int i = 0; i < 16; ++i) out[TB_A + i] = (double)A.m[i];
     for (int i = 0; i < 4; ++i) { out[TB_B + i] = (double)Bv[i]; out[TB_C + i] = (double)Cv[i]; }
     out[TB_D] = (double)D;
@@ -638,6 +643,43 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L)
             for (int k = 0; k < 4; ++k) g[k] += AB[(size_t)(i - 1) * 4 + k] * h[i - 1 - ip];
         for (int k = 0; k < 4; ++k) c[4 + k] = (double)g[k];
     }
+    /* tile tables (native_tables.tile_tables): M^(2^k), M^T, G_0, alpha_b, beta_b */
+    {
+        const LM &M = pw[L];
+        std::vector<LM> Mp(T + 1);
+        for (int i = 0; i < 16; ++i) Mp[0].m[i] = (i % 5 == 0) ? 1 : 0;
+        for (int b = 1; b <= T; ++b) Mp[b] = lm_mul(M, Mp[b - 1]);
+        std::vector<LM> G(T + 1);
+        for (int i = 0; i < 16; ++i) G[T].m[i] = 0;
+        for (int b = T - 1; b >= 0; --b) {                      /* G_b = P M^b + M G_{b+1} */
+            const LM a = lm_mul(P, Mp[b]), c = lm_mul(M, G[b + 1]);
+            for (int i = 0; i < 16; ++i) G[b].m[i] = a.m[i] + c.m[i];
+        }
+        auto rowC = [&](const LM &X, LD *r) {                   /* r = C X */
+            for (int c2 = 0; c2 < 4; ++c2) {
+                LD acc = 0;
+                for (int k = 0; k < 4; ++k) acc += Cv[k] * X.m[k * 4 + c2];
+                r[c2] = acc;
+            }
+        };
+        double *tt = &out[TB_COEF + 8 * (size_t)(L + 1)];
+        LM K = M;
+        for (int k = 0; k < 6; ++k) {
+            for (int i = 0; i < 16; ++i) tt[TT_KPOW + 16 * k + i] = (double)K.m[i];
+            K = lm_mul(K, K);
+        }
+        for (int i = 0; i < 16; ++i) { tt[TT_MT + i] = (double)Mp[T].m[i]; tt[TT_G0 + i] = (double)G[0].m[i]; }
+        for (int b = 0; b < T; ++b) {
+            LD al[4], cg[4], cm[4];
+            rowC(Mp[T - b], al);
+            rowC(G[b], cg);
+            rowC(Mp[b], cm);
+            for (int k = 0; k < 4; ++k) {
+                tt[TT_ALPHA + 4 * b + k] = (double)al[k];
+                tt[TT_BETA + 4 * b + k] = (double)(cg[k] + D * cm[k]);
+            }
+        }
+    }
     return out;
 }
 }  // namespace
@@ -651,122 +693,109 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* tables (cached on the host key; uploaded when they change) */
     /* tables and block offsets: rebuilt / re-uploaded only when they change (the
      * host copies live in the context, so the async upload never outlives them) */
-    std::vector<int64_t> key(15);
+    /* tiles of bt blocks: the int16 path's LDS tile holds <= NB_RCH*512 samples */
+    const int bt = std::min(64, (NB_RCH * 512 - 16) / ds);
+    std::vector<int64_t> key(16);
     for (int i = 0; i < 12; ++i) std::memcpy(&key[i], &P->sos[i], 8);
     key[12] = ds;
     std::memcpy(&key[13], &P->sos_zi[0], 8);
     std::memcpy(&key[14], &P->sos_zi[2], 8);
+    key[15] = bt;
     if (key != ctx->nat_key) {
-        ctx->nat_tab = build_tables(P->sos, P->sos_zi, ds);
+        ctx->nat_tab = build_tables(P->sos, P->sos_zi, ds, bt);
         ctx->nat_key = key;
         ctx->nat_tab_dirty = true;
     }
     bool grew = false;
     double *d_tab = (double *)ctx->buf("nat_tab", ctx->nat_tab.size() * 8, &rc, &grew);
     if (grew) ctx->nat_tab_dirty = true;
-    std::vector<int64_t> boff(F + 1, 0);
-    for (int f = 0; f < F; ++f) {
-        const int64_t nd = doff[f + 1] - doff[f];
-        boff[f + 1] = boff[f] + (nd > 1 ? nd - 1 : 0);
-    }
-    std::vector<int64_t> boffp(F + 1, 0);
-    for (int f = 0; f < F; ++f) boffp[f + 1] = boffp[f] + ((boff[f + 1] - boff[f] + 63) / 64) * 64;
-    const int64_t sum_blocks = boffp[F];
-    int64_t *d_boff2 = (int64_t *)ctx->buf("nat_boff", (size_t)(F + 1) * 16, &rc, &grew);
-    if (grew) ctx->nat_boff.clear();
     if (rc != BPMX_OK) return rc;
     if (ctx->nat_tab_dirty) {
         HIP_TRY(hipMemcpyAsync(d_tab, ctx->nat_tab.data(), ctx->nat_tab.size() * 8, hipMemcpyHostToDevice, s));
         ctx->nat_tab_dirty = false;
     }
-    std::vector<int64_t> both(boff);
-    both.insert(both.end(), boffp.begin(), boffp.end());
-    if (both != ctx->nat_boff) {
-        ctx->nat_boff = both;
-        HIP_TRY(hipMemcpyAsync(d_boff2, ctx->nat_boff.data(), (size_t)(F + 1) * 16, hipMemcpyHostToDevice, s));
+    const double *d_tt = d_tab + TB_COEF + 8 * (size_t)(ds + 1);
+    /* geometry: block offsets, per-file tile offsets, the tile list (cached with the context) */
+    std::vector<int64_t> tk(4 + 2 * (F + 1));
+    tk[0] = bt; tk[1] = F; tk[2] = ds; tk[3] = 0;
+    for (int f = 0; f <= F; ++f) { tk[4 + f] = foff[f]; tk[5 + F + f] = doff[f]; }
+    if (tk != ctx->nat_tkey) {
+        std::vector<int64_t> geo(2 * (F + 1), 0);             /* boff | toff */
+        std::vector<NatTile> tv;
+        for (int f = 0; f < F; ++f) {
+            const int64_t nd = doff[f + 1] - doff[f];
+            const int64_t nb = nd > 1 ? nd - 1 : 0;
+            geo[f + 1] = geo[f] + nb;
+            geo[F + 1 + f] = (int64_t)tv.size();
+            if (nd <= 15) continue;                          /* inactive (filtfilt would raise) */
+            for (int64_t j0 = 0; j0 < nb; j0 += bt)
+                tv.push_back(NatTile{foff[f] + j0 * ds, geo[f] + j0, doff[f] + j0, (int32_t)j0, (int32_t)nb, f, 0});
+        }
+        geo[2 * F + 1] = (int64_t)tv.size();
+        ctx->nat_boff = geo;
+        ctx->nat_tiles.resize(tv.size() * sizeof(NatTile));
+        if (!tv.empty()) std::memcpy(ctx->nat_tiles.data(), tv.data(), ctx->nat_tiles.size());
+        ctx->nat_tkey = tk;
+        ctx->nat_tiles_dirty = true;
     }
-    const int64_t *d_boffp = d_boff2 + F + 1;
-    double *uv = (double *)ctx->buf("nat_uv", (size_t)std::max<int64_t>(sum_blocks, 1) * 64, &rc);
-    double *S = (double *)ctx->buf("nat_S", (size_t)std::max<int64_t>(sum_blocks, 1) * 32, &rc);
+    const int64_t nt = (int64_t)(ctx->nat_tiles.size() / sizeof(NatTile));
+    const int64_t sum_blocks = ctx->nat_boff[F];
+    int64_t *d_geo = (int64_t *)ctx->buf("nat_geo", (size_t)(F + 1) * 16, &rc, &grew);
+    if (grew) ctx->nat_tiles_dirty = true;
+    NatTile *d_tiles = (NatTile *)ctx->buf("nat_tiles", std::max<size_t>(ctx->nat_tiles.size(), 64), &rc, &grew);
+    if (grew) ctx->nat_tiles_dirty = true;
+    if (rc != BPMX_OK) return rc;
+    if (ctx->nat_tiles_dirty) {
+        HIP_TRY(hipMemcpyAsync(d_geo, ctx->nat_boff.data(), (size_t)(F + 1) * 16, hipMemcpyHostToDevice, s));
+        if (nt > 0)
+            HIP_TRY(hipMemcpyAsync(d_tiles, ctx->nat_tiles.data(), ctx->nat_tiles.size(), hipMemcpyHostToDevice, s));
+        ctx->nat_tiles_dirty = false;
+    }
+    double *gam = (double *)ctx->buf("nat_gam", (size_t)std::max<int64_t>(sum_blocks, 1) * 8, &rc);
+    double *agg = (double *)ctx->buf("nat_agg", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
+    double *carry = (double *)ctx->buf("nat_carry", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
+    double *part = (double *)ctx->buf("nat_part", (size_t)F * 64 * NAT_PART * 8, &rc);
     double *tail = (double *)ctx->buf("nat_tail", (size_t)F * (ds + 16) * 8, &rc);
     double *yd = O->y ? O->y : (double *)ctx->buf("nat_yd", (size_t)doff[F] * 8, &rc);
     double2 *z = (double2 *)ctx->buf("nat_z", (size_t)doff[F] * 16, &rc);
     if (rc != BPMX_OK) return rc;
-    int64_t maxnb = 0;
-    for (int f = 0; f < F; ++f) maxnb = std::max<int64_t>(maxnb, doff[f + 1] - doff[f] - 1);
-    {
+    if (nt > 0) {
         NatBlockArgs a;
-        a.pcm = B->pcm; a.foff = d_foff; a.boff = d_boff2; a.boffp = d_boffp; a.active = d_active; a.n_files = F;
-        a.channels = P->channels; a.ds = ds; a.tab = d_tab; a.uv = uv;
+        a.pcm = B->pcm; a.tiles = d_tiles; a.n_tiles = nt; a.total = foff[F]; a.bt = bt;
+        a.channels = P->channels; a.ds = ds; a.tab = d_tab; a.tt = d_tt; a.gam = gam; a.agg = agg; a.part = part;
         const bool fast = P->dtype == BPMX_DT_I16 && P->channels == 1 && ((uintptr_t)B->pcm & 15) == 0;
-        if (maxnb > 0) {
-            if (fast) {
-                const int bt = std::min(64, (NB_RCH * 512 - 16) / ds);
-                std::vector<int64_t> tk(3 + F);
-                tk[0] = bt; tk[1] = F; tk[2] = foff[F];
-                for (int f = 0; f < F; ++f) tk[3 + f] = foff[f];
-                if (tk != ctx->nat_tkey || doff != ctx->nat_tdoff) {
-                    std::vector<NatTile> tv;
-                    for (int f = 0; f < F; ++f) {
-                        const int64_t nd = doff[f + 1] - doff[f];
-                        if (nd <= 15) continue;                      /* inactive (filtfilt would raise) */
-                        const int64_t nb = nd - 1;
-                        for (int64_t j0 = 0; j0 < nb; j0 += bt)
-                            tv.push_back(NatTile{foff[f] + j0 * ds, boffp[f], (int32_t)j0, (int32_t)nb});
-                    }
-                    ctx->nat_tiles.resize(tv.size() * sizeof(NatTile));
-                    std::memcpy(ctx->nat_tiles.data(), tv.data(), ctx->nat_tiles.size());
-                    ctx->nat_tkey = tk;
-                    ctx->nat_tdoff = doff;
-                    ctx->nat_tiles_dirty = true;
-                }
-                const int64_t nt = (int64_t)(ctx->nat_tiles.size() / sizeof(NatTile));
-                NatTile *d_tiles =
-                    (NatTile *)ctx->buf("nat_tiles", std::max<size_t>(ctx->nat_tiles.size(), 64), &rc, &grew);
-                if (rc != BPMX_OK) return rc;
-                if (grew) ctx->nat_tiles_dirty = true;
-                if (ctx->nat_tiles_dirty) {
-                    HIP_TRY(hipMemcpyAsync(d_tiles, ctx->nat_tiles.data(), ctx->nat_tiles.size(),
-                                           hipMemcpyHostToDevice, s));
-                    ctx->nat_tiles_dirty = false;
-                }
-                a.tiles = d_tiles; a.n_tiles = nt; a.total = foff[F]; a.bt = bt;
-                const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>(nt, 1), 256 * 8);
-                if (nt > 0) LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16, dim3(grid), dim3(64), 0, s, a,
-                                   (const double *)(d_tab + TB_COEF));
-            } else {
-                const dim3 g((unsigned)((maxnb + 31) / 32), F), b(64);
-                const size_t lds = ((size_t)32 * ds + 1) * 8;
+        if (fast) {
+            const unsigned grid = (unsigned)std::min<int64_t>(nt, 256 * 8);
+            LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16, dim3(grid), dim3(64), 0, s, a,
+                   (const double *)(d_tab + TB_COEF));
+        } else {
 #define NAT_GEN(DT)                                                                                        \
-    if (P->channels > 1) {                                                                                 \
-        (void)hipFuncSetAttribute((const void *)k_native_blocks_gen<DT, true>,                             \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
-        LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_gen<DT, true>), g, b, lds, s, a);               \
-    } else {                                                                                               \
-        (void)hipFuncSetAttribute((const void *)k_native_blocks_gen<DT, false>,                            \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
-        LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_gen<DT, false>), g, b, lds, s, a);              \
-    }
-                switch (P->dtype) {
-                case BPMX_DT_U8: NAT_GEN(BPMX_DT_U8) break;
-                case BPMX_DT_I16: NAT_GEN(BPMX_DT_I16) break;
-                case BPMX_DT_I32: NAT_GEN(BPMX_DT_I32) break;
-                case BPMX_DT_F32: NAT_GEN(BPMX_DT_F32) break;
-                default: NAT_GEN(BPMX_DT_F64) break;
-                }
-#undef NAT_GEN
+    if (P->channels > 1) LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_gen<DT, true>), dim3((unsigned)nt), \
+                                dim3(64), 0, s, a);                                                          \
+    else LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_gen<DT, false>), dim3((unsigned)nt), dim3(64), 0, s, a);
+            switch (P->dtype) {
+            case BPMX_DT_U8: NAT_GEN(BPMX_DT_U8) break;
+            case BPMX_DT_I16: NAT_GEN(BPMX_DT_I16) break;
+            case BPMX_DT_I32: NAT_GEN(BPMX_DT_I32) break;
+            case BPMX_DT_F32: NAT_GEN(BPMX_DT_F32) break;
+            default: NAT_GEN(BPMX_DT_F64) break;
             }
+#undef NAT_GEN
         }
     }
     {
-        NatScanArgs a;
-        a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.boff = d_boff2; a.boffp = d_boffp; a.active = d_active;
-        a.n_files = F;
-        a.dtype = P->dtype; a.channels = P->channels; a.ds = ds; a.tab = d_tab; a.uv = uv; a.S = S; a.tail = tail;
-        a.yd = yd;
+        NatCarryArgs a;
+        a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.boff = d_geo; a.toff = d_geo + F + 1;
+        a.active = d_active; a.n_files = F; a.dtype = P->dtype; a.channels = P->channels; a.ds = ds; a.bt = bt;
+        a.tab = d_tab; a.tt = d_tt; a.agg = agg; a.part = part; a.carry = carry; a.tail = tail; a.yd = yd;
         SosStep ss;
         for (int i = 0; i < 12; ++i) ss.s[i] = P->sos[i];
-        LAUNCH(ctx, s, "k_native_scan", k_native_scan, dim3(F), dim3(64), 0, s, a, ss);
+        LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
+    }
+    if (nt > 0) {
+        NatYdArgs a;
+        a.tiles = d_tiles; a.bt = bt; a.tt = d_tt; a.carry = carry; a.gam = gam; a.yd = yd;
+        LAUNCH(ctx, s, "k_native_yd", k_native_yd, dim3((unsigned)nt), dim3(64), 0, s, a);
     }
     /* Hilbert: runs of equal Nd share one batched plan */
     int f0 = 0;

@@ -139,3 +139,118 @@ def model_decimated(x_ext: np.ndarray, sos: np.ndarray, sos_zi: np.ndarray, ds: 
         c = 15 + j * ds
         out[j] = C @ Q[j] + D * (C @ S[j] + D * x_ext[c])
     return out
+
+
+TILE = 64   # blocks per k_native_blocks tile (one per lane)
+
+
+@functools.lru_cache(maxsize=32)
+def _tile_tables(sos_key: tuple, ds: int, T: int):
+    """Extended-precision tables of the tile formulation (k_native_blocks ->
+    k_native_carry -> k_native_yd), see model_tiled."""
+    A, B, C, D = state_space(np.array(sos_key))
+    L = ds
+    pw = [np.eye(4, dtype=np.longdouble)]
+    for _ in range(L + 1):
+        pw.append(A @ pw[-1])
+    M = pw[L]
+    AB = np.stack([pw[i] @ B for i in range(L + 1)])
+    P = sum(np.outer(AB[i - 1], C @ pw[i]) for i in range(1, L + 1))
+    Mp = [np.eye(4, dtype=np.longdouble)]
+    for _ in range(T):
+        Mp.append(M @ Mp[-1])                                    # Mp[b] = M^b
+    G = [None] * (T + 1)
+    G[T] = np.zeros((4, 4), dtype=np.longdouble)
+    for b in range(T - 1, -1, -1):                                # G_b = P M^b + M G_{b+1}
+        G[b] = P @ Mp[b] + M @ G[b + 1]
+    alpha = np.stack([C @ Mp[T - b] for b in range(T)])           # C M^(T-b)
+    beta = np.stack([C @ G[b] + D * (C @ Mp[b]) for b in range(T)])
+    kpow = np.stack([Mp[1 << k] for k in range(int(np.log2(T)))])  # M^1, M^2, ..., M^(T/2)
+    f64 = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    return dict(MT=f64(Mp[T]), G0=f64(G[0]), alpha=f64(alpha), beta=f64(beta), kpow=f64(kpow))
+
+
+def tile_tables(sos: np.ndarray, ds: int, T: int = TILE) -> dict:
+    return _tile_tables(tuple(float(v) for v in np.asarray(sos).ravel()), int(ds), int(T))
+
+
+def model_tiled(x_ext: np.ndarray, sos: np.ndarray, sos_zi: np.ndarray, ds: int, n: int, T: int = TILE):
+    """numpy model of the tiled kernels (test aid; must equal model_decimated):
+
+    per full tile t of T blocks (j0 = T t), lane b, with u, v the block sums:
+      incl_b = sum_{c<=b} M^(b-c) u_c,   loc_b = incl_(b-1),   w_b = P loc_b + v_b
+      R_b = sum_{c>=b} M^(c-b) w_c
+      yd_b = alpha_b . Qe_t + beta_b . S0_t + gamma_b,
+      gamma_b = C R_b + D C loc_b + D^2 x_b
+    carries (per file, sequential over tiles):
+      S0_(t+1) = M^T S0_t + incl_(T-1),   Q_start_t = M^T Qe_t + R_0 + G_0 S0_t = Qe_(t-1)
+    the partial last tile and the tail run the exact block / sample recursions."""
+    t = tables(sos, ds)
+    A, B, C, D, M, P, F, G = (t[k] for k in "ABCDMPFG")
+    tt = tile_tables(sos, ds, T)
+    zi = np.asarray(sos_zi, dtype=np.float64).ravel()
+    nd = -(-n // ds)
+    nb = nd - 1
+    ne = n + 30
+
+    def stepf(s, u):
+        return A @ s + B * u, C @ s + D * u
+
+    s = zi * x_ext[0]
+    for m in range(15):
+        s, _ = stepf(s, x_ext[m])
+    c = lambda j: 15 + j * ds
+    u = np.array([F.T @ x_ext[c(j):c(j) + ds] for j in range(nb)]).reshape(nb, 4)
+    v = np.array([G.T @ x_ext[c(j):c(j) + ds + 1] for j in range(nb)]).reshape(nb, 4)
+    xb = np.array([x_ext[c(j)] for j in range(nd)])
+    nt = nb // T
+    gam = np.zeros(nt * T)
+    aggF = np.zeros((nt, 4))
+    R0 = np.zeros((nt, 4))
+    for ti in range(nt):                                           # k_native_blocks, full tiles
+        j0 = ti * T
+        incl = np.zeros((T, 4))
+        acc = np.zeros(4)
+        for b in range(T):
+            acc = M @ acc + u[j0 + b]
+            incl[b] = acc
+        loc = np.vstack([np.zeros(4), incl[:-1]])
+        w = (P @ loc.T).T + v[j0:j0 + T]
+        R = np.zeros((T, 4))
+        acc = np.zeros(4)
+        for b in range(T - 1, -1, -1):
+            acc = M @ acc + w[b]
+            R[b] = acc
+        gam[j0:j0 + T] = R @ C + D * (loc @ C) + D * D * xb[j0:j0 + T]
+        aggF[ti] = incl[-1]
+        R0[ti] = R[0]
+    S0 = np.zeros((nt + 1, 4))                                     # k_native_carry
+    S0[0] = s
+    for ti in range(nt):
+        S0[ti + 1] = tt["MT"] @ S0[ti] + aggF[ti]
+    Sp = [S0[nt]]
+    for j in range(nt * T, nb):
+        Sp.append(M @ Sp[-1] + u[j])
+    slast = Sp[-1]
+    yf = []
+    s = slast.copy()
+    for m in range(c(nd - 1), ne):
+        s, y = stepf(s, x_ext[m])
+        yf.append(y)
+    q = zi * yf[-1]
+    for idx in range(len(yf) - 1, 0, -1):
+        q = A @ q + B * yf[idx]
+    out = np.empty(nd)
+    out[nd - 1] = C @ q + D * yf[0]
+    for j in range(nb - 1, nt * T - 1, -1):
+        Sj = Sp[j - nt * T]
+        q = M @ q + P @ Sj + v[j]
+        out[j] = C @ q + D * (C @ Sj + D * xb[j])
+    Qe = np.zeros((nt, 4))
+    for ti in range(nt - 1, -1, -1):
+        Qe[ti] = q
+        q = tt["MT"] @ q + R0[ti] + tt["G0"] @ S0[ti]
+    for ti in range(nt):                                           # k_native_yd
+        j0 = ti * T
+        out[j0:j0 + T] = tt["alpha"] @ Qe[ti] + tt["beta"] @ S0[ti] + gam[j0:j0 + T]
+    return out
