@@ -65,9 +65,9 @@ def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, 
             "k_native_carry": F * (nb // 64 * 128 + 64 * 16 * 8),  # tile carries in/out, partial tile
             "k_native_yd": F * nb * (8 + 8),                          # gamma in, yd out
             "rocfft_r2c": F * (nd * 8 + half * 16),
-            "k_hilbert_weights": F * half * 16 * 2,
-            "rocfft_c2c_inv": F * nd * 16 * 2,
-            "k_native_env": F * nd * (16 + 8),
+            "k_hilbert_rotate": F * half * 16 * 2,
+            "rocfft_c2r": F * (half * 16 + nd * 8),
+            "k_native_env": F * nd * (8 + 8 + 8),
         })
     # reference: the picked samples, y kept in scratch (written fwd, rewritten bwd, read twice), env written once
     return dict(common, **{"k_envelope_ref": F * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8)})

@@ -21,9 +21,9 @@
  *                    the partial last tile and the <= ds+15-sample tail by
  *                    exact recursion.
  *   k_native_yd      yd_j = alpha_b . Qe_t + beta_b . S0_t + gamma_j.
- *   rocFFT           R2C + C2C inverse (Hilbert), one plan per (Nd, batch).
- *   k_hilbert_weights  the analytic-signal weights h (1, 2, ..., 1, 0, ...).
- *   k_native_env     |z|/Nd and the centred rolling mean, LDS-tiled.
+ *   rocFFT           R2C + C2R (Hilbert transform), one plan pair per (Nd, batch).
+ *   k_hilbert_rotate   -i on the half spectrum (C2R of it = N x Hilbert transform).
+ *   k_native_env     |z| = sqrt(y^2 + H^2) and the centred rolling mean, LDS-tiled.
  */
 #include <rocfft/rocfft.h>
 
@@ -85,7 +85,8 @@ struct NatYdArgs {
 };
 
 struct NatEnvArgs {
-    const double2 *z;              /* [sumNd] analytic signal (unnormalised) */
+    const double *y;               /* [sumNd] decimated filtered signal (real part) */
+    const double *h;               /* [sumNd] N x Hilbert transform (unnormalised C2R) */
     const int64_t *doff;
     const int32_t *active;
     int32_t n_files, window;
@@ -453,26 +454,24 @@ __global__ __launch_bounds__(64) void k_native_yd(NatYdArgs A) {
 }
 
 /* ---------------------------------------------------------------------- */
-/* analytic-signal weights on the R2C half spectrum, written as a full-length
- * complex spectrum in place (slot of Nd complex values per file) */
-__global__ __launch_bounds__(256) void k_hilbert_weights(double2 *z, const int64_t *doff, const int32_t *active,
-                                                         int f_begin, int f_end) {
+/* Hilbert transform on the R2C half spectrum: W_k = -i Y_k for 0 < k < N/2,
+ * W_0 = W_(N/2) = 0.  A C2R of W gives N * Im(analytic signal): scipy's
+ * hilbert (ifft(fft(x) * h), h = 1, 2, ..., 2, [1], 0, ...) has imaginary part
+ * (2/N) Re sum_(0<k<N/2) (-i X_k) e^(2 pi i k n / N), and X_0, X_(N/2) are real. */
+__global__ __launch_bounds__(256) void k_hilbert_rotate(double2 *z, const int64_t *doff, const int32_t *active,
+                                                        int f_begin, int f_end) {
     const int f = f_begin + blockIdx.y;
     if (f >= f_end || !active[f]) return;
     const int64_t n = doff[f + 1] - doff[f];
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
+    if (k > n / 2) return;
     double2 *zf = z + doff[f];
-    double w;
-    if (k == 0) w = 1.0;
-    else if ((n % 2 == 0) && k == n / 2) w = 1.0;
-    else if (k < (n + 1) / 2) w = 2.0;
-    else w = 0.0;
-    if (w == 0.0) zf[k] = make_double2(0.0, 0.0);
-    else if (w == 2.0) { double2 c = zf[k]; zf[k] = make_double2(2.0 * c.x, 2.0 * c.y); }
+    const double2 c = zf[k];
+    zf[k] = (k == 0 || 2 * k == n) ? make_double2(0.0, 0.0) : make_double2(c.y, -c.x);
 }
 
-/* |z|/Nd and the centred rolling mean (window w, min_periods 1) */
+/* |z| = sqrt(y^2 + (h/N)^2) (h: unnormalised C2R output) and the centred
+ * rolling mean (window w, min_periods 1), LDS-tiled */
 constexpr int NE_T = 256;
 __global__ __launch_bounds__(NE_T) void k_native_env(NatEnvArgs A) {
     __shared__ double mag[NE_T + 2 * 1024];
@@ -484,11 +483,11 @@ __global__ __launch_bounds__(NE_T) void k_native_env(NatEnvArgs A) {
     const int64_t w = A.window, off = (w - 1) / 2;
     const int64_t lo = i0 + 1 + off - w < 0 ? 0 : i0 + 1 + off - w;
     const int64_t hiE = i0 + NE_T + off < n ? i0 + NE_T + off : n;   /* exclusive */
-    const double2 *z = A.z + A.doff[f];
+    const double *y = A.y + A.doff[f], *h = A.h + A.doff[f];
     const double inv = 1.0 / (double)n;
     for (int64_t p = lo + threadIdx.x; p < hiE; p += NE_T) {
-        const double2 c = z[p];
-        mag[p - lo] = sqrt(c.x * c.x + c.y * c.y) * inv;
+        const double re = y[p], im = h[p] * inv;
+        mag[p - lo] = sqrt(re * re + im * im);
     }
     __syncthreads();
     const int64_t i = i0 + threadIdx.x;
@@ -535,13 +534,13 @@ int get_plans(int dev, int64_t nd, int64_t batch, FftPlans **out) {
                             rocfft_precision_double, 1, &len, (size_t)batch, d1);
     if (st != rocfft_status_success) return fft_fail("plan_create(r2c)", st);
     if ((st = rocfft_plan_description_create(&d2)) != rocfft_status_success) return fft_fail("plan_description", st);
-    st = rocfft_plan_description_set_data_layout(d2, rocfft_array_type_complex_interleaved,
-                                                 rocfft_array_type_complex_interleaved, nullptr, nullptr, 1, nullptr,
-                                                 len, 1, nullptr, len);
-    if (st != rocfft_status_success) return fft_fail("set_data_layout(c2c)", st);
-    st = rocfft_plan_create(&p.inv, rocfft_placement_inplace, rocfft_transform_type_complex_inverse,
+    st = rocfft_plan_description_set_data_layout(d2, rocfft_array_type_hermitian_interleaved,
+                                                 rocfft_array_type_real, nullptr, nullptr, 1, nullptr, len, 1,
+                                                 nullptr, len);
+    if (st != rocfft_status_success) return fft_fail("set_data_layout(c2r)", st);
+    st = rocfft_plan_create(&p.inv, rocfft_placement_notinplace, rocfft_transform_type_real_inverse,
                             rocfft_precision_double, 1, &len, (size_t)batch, d2);
-    if (st != rocfft_status_success) return fft_fail("plan_create(c2c)", st);
+    if (st != rocfft_status_success) return fft_fail("plan_create(c2r)", st);
     rocfft_plan_description_destroy(d1);
     rocfft_plan_description_destroy(d2);
     size_t w1 = 0, w2 = 0;
@@ -758,6 +757,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     double *tail = (double *)ctx->buf("nat_tail", (size_t)F * (ds + 16) * 8, &rc);
     double *yd = O->y ? O->y : (double *)ctx->buf("nat_yd", (size_t)doff[F] * 8, &rc);
     double2 *z = (double2 *)ctx->buf("nat_z", (size_t)doff[F] * 16, &rc);
+    double *hb = (double *)ctx->buf("nat_h", (size_t)doff[F] * 8, &rc);
     if (rc != BPMX_OK) return rc;
     if (nt > 0) {
         NatBlockArgs a;
@@ -820,12 +820,13 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 if (st != rocfft_status_success) { rocfft_execution_info_destroy(info); return fft_fail("rocfft_execute(r2c)", st); }
                 if ((rc = l.done()) != BPMX_OK) { rocfft_execution_info_destroy(info); return rc; }
             }
-            LAUNCH(ctx, s, "k_hilbert_weights", k_hilbert_weights, dim3((unsigned)((nd + 255) / 256), f1 - f0),
+            LAUNCH(ctx, s, "k_hilbert_rotate", k_hilbert_rotate, dim3((unsigned)((nd / 2 + 256) / 256), f1 - f0),
                    dim3(256), 0, s, z, d_doff, d_active, f0, f1);
             {
-                Launch l(ctx, s, "rocfft_c2c_inv");
-                rocfft_status st = rocfft_execute(pl->inv, out, nullptr, info);
-                if (st != rocfft_status_success) { rocfft_execution_info_destroy(info); return fft_fail("rocfft_execute(c2c)", st); }
+                Launch l(ctx, s, "rocfft_c2r");
+                void *hout[1] = {hb + doff[f0]};
+                rocfft_status st = rocfft_execute(pl->inv, out, hout, info);
+                if (st != rocfft_status_success) { rocfft_execution_info_destroy(info); return fft_fail("rocfft_execute(c2r)", st); }
                 if ((rc = l.done()) != BPMX_OK) { rocfft_execution_info_destroy(info); return rc; }
             }
             rocfft_execution_info_destroy(info);
@@ -835,7 +836,8 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     {
         if (P->env_window > 2 * 1024) return fail(BPMX_E_LIMIT, "envelope window too large for k_native_env");
         NatEnvArgs a;
-        a.z = z; a.doff = d_doff; a.active = d_active; a.n_files = F; a.window = P->env_window; a.env = O->env;
+        a.y = yd; a.h = hb; a.doff = d_doff; a.active = d_active; a.n_files = F; a.window = P->env_window;
+        a.env = O->env;
         LAUNCH(ctx, s, "k_native_env", k_native_env, dim3((unsigned)((maxnd + NE_T - 1) / NE_T), F), dim3(NE_T), 0,
                s, a);
     }
