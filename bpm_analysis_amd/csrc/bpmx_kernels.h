@@ -59,6 +59,9 @@ struct PeakArgs {
     int32_t *nout;         /* [F] */
     int32_t *run_out;      /* optional [F]: 1 if nout >= run_min */
     int32_t run_min;
+#ifdef BPMX_STAMPS
+    unsigned long long *stamps;
+#endif
 };
 
 struct InterpArgs {

@@ -24,6 +24,7 @@
  */
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
+#include "bpmx_stamps.h"
 
 namespace bpmx {
 
@@ -124,24 +125,39 @@ __global__ __launch_bounds__(256) void k_block_stats(BlockStatArgs A) {
 
 /* ------------------------------------------------------------------------ */
 /* prominence of peak p (value xp = sg*e[p]) — _peak_prominences, wlen = -1:
- * min of x over (left_higher, p] and [p, right_higher), prom = xp - max(...) */
-__device__ double prominence_wave(const double *e, double sg, int64_t n, const double *bmx, const double *bmn,
-                                  int64_t p, double xp) {
+ * min of x over (left_higher, p] and [p, right_higher), prom = xp - max(...).
+ * One wave; at most two dependent rounds of global loads: p's own 64-sample
+ * block (shared by both sides), then — for a side whose higher sample lies
+ * beyond it — the block found by walking the block max tables (LDS). */
+template <int NP>
+__device__ void prominence_waves(const double *e, double sg, int64_t n, const double *bmx, const double *bmn,
+                                 const int64_t *pp, const double *xpp, double *prom) {
     const int lane = lane_id();
     const int64_t nb = (n + 63) >> 6;
     const double INF = __builtin_inf();
-    const int64_t blk = p >> 6;
-    double lmin, rmin;
-    {   /* left */
+    double v[NP], lm[NP], rm[NP];
+    int64_t qL[NP], qR[NP];
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {             /* first round of loads: each peak's own block */
+        const int64_t pos = ((pp[c] >> 6) << 6) + lane;
+        v[c] = (pp[c] >= 0 && pos < n) ? sg * e[pos] : -INF;
+    }
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {
+        const int64_t p = pp[c];
+        const double xp = xpp[c];
+        const int64_t blk = p >> 6;
         const int64_t pos = (blk << 6) + lane;
-        const bool valid = pos <= p;
-        const double v = valid ? sg * e[pos] : -INF;
-        const unsigned long long m = __ballot(valid && v > xp);
-        if (m) {
-            const int L = 63 - __clzll(m);
-            lmin = wave_min((valid && lane > L) ? v : INF);
+        qL[c] = qR[c] = -1;
+        lm[c] = rm[c] = INF;
+        if (p < 0) continue;                   /* uniform: empty slot */
+        const unsigned long long mL = __ballot(pos <= p && v[c] > xp);
+        const unsigned long long mR = __ballot(pos >= p && pos < n && v[c] > xp);
+        if (mL) {
+            const int L = 63 - __clzll(mL);
+            lm[c] = (pos <= p && lane > L) ? v[c] : INF;
         } else {
-            lmin = wave_min(valid ? v : INF);
+            lm[c] = pos <= p ? v[c] : INF;
             for (int64_t bs = blk - 1; bs >= 0; bs -= 64) {
                 const int64_t b = bs - lane;
                 const bool vb = b >= 0;
@@ -150,28 +166,18 @@ __device__ double prominence_wave(const double *e, double sg, int64_t n, const d
                 const unsigned long long mb = __ballot(vb && bm > xp);
                 if (mb) {
                     const int Lb = __ffsll((long long)mb) - 1;
-                    lmin = fmin(lmin, wave_min(lane < Lb ? bn : INF));
-                    const int64_t q = ((bs - Lb) << 6) + lane;      /* a full block left of p */
-                    const double v2 = sg * e[q];
-                    const unsigned long long m2 = __ballot(v2 > xp);
-                    const int L2 = 63 - __clzll(m2);
-                    lmin = fmin(lmin, wave_min(lane > L2 ? v2 : INF));
+                    lm[c] = fmin(lm[c], lane < Lb ? bn : INF);
+                    qL[c] = bs - Lb;
                     break;
                 }
-                lmin = fmin(lmin, wave_min(bn));
+                lm[c] = fmin(lm[c], bn);
             }
         }
-    }
-    {   /* right */
-        const int64_t pos = (blk << 6) + lane;
-        const bool valid = pos >= p && pos < n;
-        const double v = valid ? sg * e[pos] : -INF;
-        const unsigned long long m = __ballot(valid && v > xp);
-        if (m) {
-            const int R = __ffsll((long long)m) - 1;
-            rmin = wave_min((valid && lane < R) ? v : INF);
+        if (mR) {
+            const int R = __ffsll((long long)mR) - 1;
+            rm[c] = (pos >= p && pos < n && lane < R) ? v[c] : INF;
         } else {
-            rmin = wave_min(valid ? v : INF);
+            rm[c] = (pos >= p && pos < n) ? v[c] : INF;
             for (int64_t bs = blk + 1; bs < nb; bs += 64) {
                 const int64_t b = bs + lane;
                 const bool vb = b < nb;
@@ -180,20 +186,43 @@ __device__ double prominence_wave(const double *e, double sg, int64_t n, const d
                 const unsigned long long mb = __ballot(vb && bm > xp);
                 if (mb) {
                     const int Rb = __ffsll((long long)mb) - 1;
-                    rmin = fmin(rmin, wave_min(lane < Rb ? bn : INF));
-                    const int64_t q = ((bs + Rb) << 6) + lane;
-                    const bool vq = q < n;
-                    const double v2 = vq ? sg * e[q] : -INF;
-                    const unsigned long long m2 = __ballot(vq && v2 > xp);
-                    const int R2 = __ffsll((long long)m2) - 1;
-                    rmin = fmin(rmin, wave_min((vq && lane < R2) ? v2 : INF));
+                    rm[c] = fmin(rm[c], lane < Rb ? bn : INF);
+                    qR[c] = bs + Rb;
                     break;
                 }
-                rmin = fmin(rmin, wave_min(bn));
+                rm[c] = fmin(rm[c], bn);
             }
         }
     }
-    return xp - fmax(lmin, rmin);
+    double vl[NP], vr[NP];
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {             /* second round: the far blocks, all at once */
+        const int64_t ql = (qL[c] << 6) + lane, qr = (qR[c] << 6) + lane;
+        vl[c] = qL[c] >= 0 ? sg * e[ql] : -INF;
+        vr[c] = (qR[c] >= 0 && qr < n) ? sg * e[qr] : -INF;
+    }
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {
+        const double xp = xpp[c];
+        if (qL[c] >= 0) {
+            const int L2 = 63 - __clzll(__ballot(vl[c] > xp));
+            lm[c] = fmin(lm[c], lane > L2 ? vl[c] : INF);
+        }
+        if (qR[c] >= 0) {
+            const int64_t qr = (qR[c] << 6) + lane;
+            const int R2 = __ffsll((long long)__ballot(qr < n && vr[c] > xp)) - 1;
+            rm[c] = fmin(rm[c], (qr < n && lane < R2) ? vr[c] : INF);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int c = 0; c < NP; ++c) {
+            lm[c] = fmin(lm[c], __shfl_xor(lm[c], o));
+            rm[c] = fmin(rm[c], __shfl_xor(rm[c], o));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NP; ++c) prom[c] = xpp[c] - fmax(lm[c], rm[c]);
 }
 
 enum { ST_UNDECIDED = 0, ST_KEPT = 1, ST_REMOVED = 2, ST_FINAL = 3 };
@@ -206,8 +235,10 @@ __device__ __forceinline__ void st_state(uint8_t *p, uint8_t v) {
 }
 
 constexpr int FP_T = 1024;
+constexpr int FP_NBMAX = 2048;   /* block tables staged in LDS up to 131072 samples */
+constexpr int FP_MC = 2048;      /* candidates kept in LDS up to this many */
 
-__global__ __launch_bounds__(FP_T) void k_find_peaks(PeakArgs A) {
+__global__ __launch_bounds__(FP_T, 8) void k_find_peaks(PeakArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f]) return;
     const int64_t d0 = A.doff[f];
@@ -215,36 +246,104 @@ __global__ __launch_bounds__(FP_T) void k_find_peaks(PeakArgs A) {
     const double *e = A.env + d0;
     const double *h = A.height ? A.height + d0 : nullptr;
     const double sg = A.sign;
-    int32_t *cand = A.cand + d0;
-    uint8_t *st = A.state + d0;
     const int tid = threadIdx.x;
     __shared__ int sh[FP_T / 64 + 1];
     __shared__ int s_flag;
+    __shared__ double s_bmx[FP_NBMAX], s_bmn[FP_NBMAX];
+    __shared__ double s_cv[FP_MC];
+    __shared__ int32_t s_cp[FP_MC];
+    __shared__ uint8_t s_st[FP_MC];
+    STAMP_DECL
 
-    /* (1)+(2) local maxima with plateau midpoints, height filter */
+    /* block tables into LDS (the prominence walks read them) */
+    const int64_t nblk = (n + 63) >> 6;
+    const double *bmx = A.bmax + A.boff[f], *bmn = A.bmin + A.boff[f];
+    if (nblk <= FP_NBMAX) {
+        for (int64_t b = tid; b < nblk; b += FP_T) { s_bmx[b] = bmx[b]; s_bmn[b] = bmn[b]; }
+        bmx = s_bmx;
+        bmn = s_bmn;
+    }
+
+    STAMP(0);
+    /* (1)+(2) local maxima with plateau midpoints, height filter.  Position
+     * i = 1 + (g*FP_G + it)*FP_T + tid; a group of FP_G iterations issues its
+     * loads together, then one (iteration, wave)-ordered scan places the hits. */
+    constexpr int FP_G = 8;
+    __shared__ int s_gc[FP_G][FP_T / 64];
     int m = 0;
-    for (int64_t c0 = 1; c0 < n - 1; c0 += FP_T) {
-        const int64_t i = c0 + tid;
-        bool is = false;
-        int64_t p = 0;
-        if (i < n - 1) {
-            const double xi = sg * e[i];
-            if (sg * e[i - 1] < xi) {
-                int64_t ia = i + 1;
-                while (ia < n - 1 && sg * e[ia] == xi) ia++;
-                if (sg * e[ia] < xi) {
-                    p = (i + ia - 1) >> 1;
-                    is = true;
-                    if (h && !(h[p] <= sg * e[p])) is = false;
+    const int64_t iters = n > 2 ? (n - 2 + FP_T - 1) / FP_T : 0;
+    int32_t *cp_g = A.cand + d0;
+    for (int64_t g0 = 0; g0 < iters; g0 += FP_G) {
+        int32_t pk[FP_G];
+        unsigned hits = 0;
+#pragma unroll
+        for (int it = 0; it < FP_G; ++it) {
+            const int64_t i = 1 + (g0 + it) * FP_T + tid;
+            pk[it] = 0;
+            if (g0 + it < iters && i < n - 1) {
+                const double xi = sg * e[i];
+                if (sg * e[i - 1] < xi) {
+                    int64_t ia = i + 1;
+                    while (ia < n - 1 && sg * e[ia] == xi) ia++;
+                    if (sg * e[ia] < xi) {
+                        const int64_t p = (i + ia - 1) >> 1;
+                        if (!h || h[p] <= sg * e[p]) { hits |= 1u << it; pk[it] = (int32_t)p; }
+                    }
                 }
             }
         }
-        int tot;
-        const int off = block_scan_flag<FP_T>(is, sh, &tot);
-        if (is) cand[m + off] = (int32_t)p;
-        m += tot;
+#pragma unroll
+        for (int it = 0; it < FP_G; ++it) {
+            const unsigned long long bal = __ballot((hits >> it) & 1u);
+            if (lane_id() == 0) s_gc[it][wave_id()] = __popcll(bal);
+        }
+        __syncthreads();
+        if (wave_id() == 0) {                                /* exclusive scan over FP_G x 16 counts */
+            constexpr int NE = FP_G * (FP_T / 64);
+            int v[NE / 64], sum = 0;
+#pragma unroll
+            for (int u = 0; u < NE / 64; ++u) {
+                v[u] = (&s_gc[0][0])[lane_id() * (NE / 64) + u];
+                sum += v[u];
+            }
+            int x = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (lane_id() >= o) x += y;
+            }
+            int run = x - sum;
+#pragma unroll
+            for (int u = 0; u < NE / 64; ++u) {
+                (&s_gc[0][0])[lane_id() * (NE / 64) + u] = run;
+                run += v[u];
+            }
+            if (lane_id() == 63) s_flag = x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < FP_G; ++it) {
+            const unsigned long long bal = __ballot((hits >> it) & 1u);
+            if ((hits >> it) & 1u) {
+                const int k = m + s_gc[it][wave_id()] + __popcll(bal & ((1ull << lane_id()) - 1ull));
+                cp_g[k] = pk[it];
+            }
+        }
+        m += s_flag;
+        __syncthreads();
+    }
+    const bool lds = m <= FP_MC;
+    int32_t *cp = lds ? s_cp : cp_g;
+    uint8_t *st = lds ? s_st : A.state + d0;
+    if (lds) {
+        for (int j = tid; j < m; j += FP_T) {
+            const int32_t p = cp_g[j];
+            s_cp[j] = p;
+            s_cv[j] = sg * e[p];
+        }
     }
     __syncthreads();
+    STAMP(1);
+    auto cval = [&](int k) { return lds ? s_cv[k] : sg * e[cp[k]]; };
 
     /* (3) distance: rounds of local decisions */
     const int64_t dist = A.distance;
@@ -259,19 +358,19 @@ __global__ __launch_bounds__(FP_T) void k_find_peaks(PeakArgs A) {
             bool pending = false;
             for (int j = tid; j < m; j += FP_T) {
                 if (ld_state(&st[j]) != ST_UNDECIDED) continue;
-                const int64_t pj = cand[j];
-                const double vj = sg * e[pj];
+                const int64_t pj = cp[j];
+                const double vj = cval(j);
                 bool killed = false, blocked = false;
-                for (int k = j - 1; k >= 0 && pj - cand[k] < dist; --k) {
-                    if (sg * e[cand[k]] > vj) {          /* earlier index wins only when strictly higher */
+                for (int k = j - 1; k >= 0 && pj - cp[k] < dist; --k) {
+                    if (cval(k) > vj) {                  /* earlier index wins only when strictly higher */
                         const uint8_t s = ld_state(&st[k]);
                         if (s == ST_KEPT) { killed = true; break; }
                         if (s == ST_UNDECIDED) blocked = true;
                     }
                 }
                 if (!killed) {
-                    for (int k = j + 1; k < m && cand[k] - pj < dist; ++k) {
-                        if (sg * e[cand[k]] >= vj) {     /* later index wins ties (stable argsort order) */
+                    for (int k = j + 1; k < m && cp[k] - pj < dist; ++k) {
+                        if (cval(k) >= vj) {             /* later index wins ties (stable argsort order) */
                             const uint8_t s = ld_state(&st[k]);
                             if (s == ST_KEPT) { killed = true; break; }
                             if (s == ST_UNDECIDED) blocked = true;
@@ -290,32 +389,56 @@ __global__ __launch_bounds__(FP_T) void k_find_peaks(PeakArgs A) {
         }
     }
 
+    STAMP(2);
     /* (4) prominences of the kept candidates, one wave each */
     const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
-    const double *bmx = A.bmax + A.boff[f], *bmn = A.bmin + A.boff[f];
-    for (int j = wave_id(); j < m; j += FP_T / 64) {
-        if (ld_state(&st[j]) != ST_KEPT) continue;
-        const int64_t p = cand[j];
-        const double prom = prominence_wave(e, sg, n, bmx, bmn, p, sg * e[p]);
-        if (lane_id() == 0) st_state(&st[j], thr <= prom ? ST_FINAL : ST_REMOVED);
+    /* the kept candidates are taken NP at a time per wave so that their global
+     * loads overlap */
+    constexpr int NP = 2;
+    {
+        const int nw = FP_T / 64, wv = wave_id();
+        int j = wv;
+        for (;;) {
+            int64_t pp[NP];
+            double xp[NP], pr[NP];
+            int jj[NP];
+#pragma unroll
+            for (int c = 0; c < NP; ++c) {
+                while (j < m && ld_state(&st[j]) != ST_KEPT) j += nw;
+                jj[c] = j < m ? j : -1;
+                pp[c] = j < m ? cp[j] : -1;
+                xp[c] = j < m ? cval(j) : 0.0;
+                j += nw;
+            }
+            if (jj[0] < 0) break;
+            prominence_waves<NP>(e, sg, n, bmx, bmn, pp, xp, pr);
+            if (lane_id() == 0) {
+#pragma unroll
+                for (int c = 0; c < NP; ++c)
+                    if (jj[c] >= 0) st_state(&st[jj[c]], thr <= pr[c] ? ST_FINAL : ST_REMOVED);
+            }
+        }
     }
     __syncthreads();
+    STAMP(3);
 
     /* (5) ordered compaction */
     int64_t *out = A.out + d0;
     int w = 0;
-    for (int c0 = 0; c0 < m; c0 += FP_T) {
-        const int j = c0 + tid;
+    for (int q0 = 0; q0 < m; q0 += FP_T) {
+        const int j = q0 + tid;
         const bool keep = j < m && ld_state(&st[j]) == ST_FINAL;
         int tot;
         const int off = block_scan_flag<FP_T>(keep, sh, &tot);
-        if (keep) out[w + off] = cand[j];
+        if (keep) out[w + off] = cp[j];
         w += tot;
     }
     if (tid == 0) {
         A.nout[f] = w;
         if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
     }
+    STAMP(4);
+    STAMP_FLUSH(A.stamps);
 }
 
 }  // namespace bpmx

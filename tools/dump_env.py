@@ -1,0 +1,23 @@
+"""Write gpurun_out/env.bin: native-mode envelopes of the bench workload (for tools/fpbench)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bpm_analysis_amd import DEFAULT_PARAMS, _native as N  # noqa: E402
+from bpm_analysis_amd.engine import Detector  # noqa: E402
+
+F, fs, n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024, 44100, 44100 * 60
+det = Detector(0)
+fo = np.arange(F + 1, dtype=np.int64) * n
+pcm = det.synth(fo, fs, 1, seed0=0)
+params = dict(DEFAULT_PARAMS)
+res = det.run(pcm, fo, fs, params, mode="native", stages=N.STAGE_ENVELOPE)
+env = res.env.cpu().numpy()
+nd = len(env) // F
+os.makedirs("gpurun_out", exist_ok=True)
+with open("gpurun_out/env.bin", "wb") as fh:
+    np.array([F, nd], dtype=np.int64).tofile(fh)
+    env.astype(np.float64).tofile(fh)
+print("wrote", F, nd)
