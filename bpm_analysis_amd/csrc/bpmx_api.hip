@@ -297,15 +297,14 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
     uint8_t *state = (uint8_t *)ctx->buf("state", (size_t)sumnd, &rc);
     if (rc != BPMX_OK) return rc;
-    {
-        BlockStatArgs a;
-        a.env = O->env; a.doff = d_doff; a.boff = d_boff; a.active = d_active; a.n_files = F;
-        a.bmax = bmax; a.bmin = bmin;
-        LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F), dim3(256), 0, s, a);
-    }
+    BlockStatArgs bs;
+    bs.env = O->env; bs.doff = d_doff; bs.boff = d_boff; bs.active = d_active; bs.n_files = F;
+    bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
+    const bool long_files = maxnd > QR_MAX;
+    if (long_files) LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F), dim3(256), 0, s, bs);
     {
         QuantArgs a;
-        a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv;
+        a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
         int L = 0;
         auto add = [&](double q, int slot) {      /* one radix select per distinct level */
             for (int l = 0; l < L; ++l)
@@ -315,7 +314,8 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->noise_floor_q, Q_NOISE); add(P->fallback_q, Q_FALLBACK); }
         if (do_peaks) add(P->peak_prom_q, Q_PEAK);
         a.n_levels = L;
-        LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(256), 0, s, a);
+        LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
+        if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(256), 0, s, a);
     }
 
     /* ---- FLOOR ---- */

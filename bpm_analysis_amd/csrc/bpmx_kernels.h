@@ -31,6 +31,7 @@ struct QuantArgs {
     int32_t slot[Q_SLOTS];  /* bitmask of the qv slots level l fills */
     double q[Q_SLOTS];
     double *qv;             /* [F][Q_SLOTS] */
+    int64_t skip_le;        /* k_quantile: files with n <= skip_le are done by k_quantile_reg */
 };
 
 struct BlockStatArgs {
@@ -40,7 +41,14 @@ struct BlockStatArgs {
     const int32_t *active;
     int32_t n_files;
     double *bmax, *bmin;
+    int64_t skip_le;        /* k_block_stats: files with n <= skip_le are done by k_quantile_reg */
 };
+
+/* one workgroup per recording with all of env in registers (n <= QR_MAX):
+ * every radix-select pass and the block max/min tables from one HBM read */
+constexpr int QR_T = 1024;
+constexpr int QR_IT = 24;
+constexpr int64_t QR_MAX = (int64_t)QR_T * QR_IT;
 
 struct PeakArgs {
     const double *env;
@@ -127,6 +135,7 @@ constexpr int RQ_T = 256;   /* outputs per tile = threads per workgroup */
 template <int DT, bool MULTI>
 __global__ void k_envelope_ref_t(EnvRefArgs A);
 __global__ void k_quantile(QuantArgs A);
+__global__ void k_quantile_reg(QuantArgs A, BlockStatArgs B);
 __global__ void k_block_stats(BlockStatArgs A);
 __global__ void k_find_peaks(PeakArgs A);
 __global__ void k_interp(InterpArgs A);

@@ -207,7 +207,6 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
         WmRec *row = lv + l * NR;
         /* ones among this wave's words (ballots are wave-uniform: scalar sums) */
         uint32_t wones = 0;
-#pragma unroll 6
         for (int w = wb; w < we; ++w) {
             const int p = w * 64 + lane;
             wones += (uint32_t)__popcll(__ballot(p < m && ((seqA[p] >> l) & 1)));
@@ -226,7 +225,6 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
             s_Z[l] = Z;
         }
         /* stable partition (zeros, then ones) and the rank directory */
-#pragma unroll 6
         for (int w = wb; w < we; ++w) {
             const int p = w * 64 + lane;
             const uint32_t v = p < m ? seqA[p] : 0u;
