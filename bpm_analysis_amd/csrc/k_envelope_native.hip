@@ -73,7 +73,6 @@ struct NatCarryArgs {
     const double *tab, *tt, *agg;
     double *part;                  /* partial-tile blocks; k_native_carry adds their states */
     double *carry;                 /* [n_tiles][8]: S0_t, Qe_t */
-    double *tail;                  /* [F][ds+16] */
     double *yd;
 };
 
@@ -372,72 +371,117 @@ __global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
  *   tail  [c_(nd-1), ne): exact forward then backward per-sample recursion
  *         -> Q at block nb and yd[nd-1];
  *   tiles Qe_t stored, Q_start = M^T Qe_t + R0_t + G0 S0_t (backward). */
+constexpr int NC_CH = 64;             /* tiles per LDS chunk of the carry walks (small: many waves per CU) */
 __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS) {
     const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f] || threadIdx.x != 0) return;
+    if (f >= A.n_files || !A.active[f]) return;
+    const int lane = threadIdx.x;
     const int64_t nd = A.doff[f + 1] - A.doff[f];
     const int64_t nb = nd - 1;
+    const int ds = A.ds, bt = A.bt;
+    const int64_t t0 = A.toff[f];
+    const int64_t Tf = nb / bt;                             /* full tiles */
+    /* Everything lane 0's sequential recursions read comes through LDS first
+     * (plain ds_read, no aliasing with the stores): tile sums / carries in
+     * chunks of NC_CH tiles, the head's 16 samples, the tail's <= ds+1 samples
+     * (+16 for the mirror), the partial tile's block records. */
+    __shared__ double s_in[NC_CH * 8], s_out[NC_CH * 8];
+    __shared__ double s_head[16], s_tail[320 + 20], s_ytl[320 + 20], s_part[64 * NAT_PART];
     const int64_t n = A.foff[f + 1] - A.foff[f];
     const int64_t fb = A.foff[f];
-    const int ds = A.ds, bt = A.bt;
+    const int64_t base = (nd - 1) * ds;                     /* x index of c_{nd-1} */
+    const int64_t ntl = n - base;                           /* real tail samples (<= ds + 1) */
+    const int Lp = (int)(nb - Tf * bt);                     /* blocks in the partial tile */
+    const int64_t tlo = n - 17 < base ? n - 17 : base;      /* mirror reads reach x[n-17] */
+    for (int k = lane; k < 16; k += 64) s_head[k] = frame_value(A.pcm, A.dtype, A.channels, fb + k);
+    for (int64_t k = lane; k < n - tlo; k += 64) s_tail[k] = frame_value(A.pcm, A.dtype, A.channels, fb + tlo + k);
+    for (int k = lane; k < Lp * NAT_PART; k += 64) s_part[k] = A.part[(int64_t)f * 64 * NAT_PART + k];
     const int wdt = work_dtype(A.dtype, A.channels);
     const double *tb = A.tab, *tt = A.tt;
     const M4 Mm = nat_ld16(tb + TB_M), Pm = nat_ld16(tb + TB_P), MT = nat_ld16(tt + TT_MT), G0 = nat_ld16(tt + TT_G0);
     const V4 Cv = nat_ld4(tb + TB_C);
     const double Dd = tb[TB_D];
     const V4 zi = nat_ld4(tb + TB_ZI);
-    auto x = [&](int64_t k) { return frame_value(A.pcm, A.dtype, A.channels, fb + k); };
+    const double *agg = A.agg + t0 * 8;
+    double *car = A.carry + t0 * 8;
     double *yd = A.yd + A.doff[f];
 
-    V4 S;
-    {
-        const double x0 = x(0);
-        const double e0 = odd_ext(wdt, x0, x(15));
+    /* head: 15 padded samples -> S at block 0 */
+    V4 S{0, 0, 0, 0};
+    __syncthreads();
+    if (lane == 0) {
+        const double x0 = s_head[0];
+        const double e0 = odd_ext(wdt, x0, s_head[15]);
         V4 z{zi.a * e0, zi.b * e0, zi.c * e0, zi.d * e0};
-        for (int k = 0; k < 15; ++k) (void)SS.step(z, odd_ext(wdt, x0, x(15 - k)));
+        for (int k = 0; k < 15; ++k) (void)SS.step(z, odd_ext(wdt, x0, s_head[15 - k]));
         S = z;
     }
-    const int64_t t0 = A.toff[f];
-    const int64_t Tf = nb / bt;                             /* full tiles */
-    const int Lp = (int)(nb - Tf * bt);                     /* blocks in the partial tile */
-    for (int64_t t = t0; t < t0 + Tf; ++t) {
-        double *c = A.carry + t * 8;
-        c[0] = S.a; c[1] = S.b; c[2] = S.c; c[3] = S.d;
-        S = add4(mv(MT, S), nat_ld4(A.agg + t * 8));
+    /* forward tile carries: car[t][0..3] = S0_t */
+    for (int64_t c0 = 0; c0 < Tf; c0 += NC_CH) {
+        const int cn = (int)(Tf - c0 < NC_CH ? Tf - c0 : NC_CH);
+        for (int k = lane; k < cn * 8; k += 64) s_in[k] = agg[c0 * 8 + k];
+        __syncthreads();
+        if (lane == 0) {
+            for (int t = 0; t < cn; ++t) {
+                s_out[t * 4 + 0] = S.a; s_out[t * 4 + 1] = S.b; s_out[t * 4 + 2] = S.c; s_out[t * 4 + 3] = S.d;
+                S = add4(mv(MT, S), V4{s_in[t * 8], s_in[t * 8 + 1], s_in[t * 8 + 2], s_in[t * 8 + 3]});
+            }
+        }
+        __syncthreads();
+        for (int k = lane; k < cn * 4; k += 64) car[(c0 + k / 4) * 8 + (k & 3)] = s_out[k];
+        __syncthreads();
     }
-    double *pp = A.part + (int64_t)f * 64 * NAT_PART;
-    for (int b = 0; b < Lp; ++b) {
-        double *r = pp + b * NAT_PART;
-        r[12] = S.a; r[13] = S.b; r[14] = S.c; r[15] = S.d;
-        S = add4(mv(Mm, S), nat_ld4(r));
-    }
-    /* tail [c_{nd-1}, ne): exact forward then backward recursion */
-    double *tl = A.tail + (int64_t)f * (ds + 16);
-    const int64_t base = (nd - 1) * ds;                     /* x index of c_{nd-1} */
-    const int64_t nt = n - base + 15;                       /* tail length incl. right pad */
-    const double xl = x(n - 1);
-    {
-        V4 z = S;
-        for (int64_t k = 0; k < nt; ++k) {
-            const int64_t xi = base + k;
-            const double u = xi < n ? x(xi) : odd_ext(wdt, xl, x(n - 2 - (xi - n)));
-            tl[k] = SS.step(z, u);
+    /* partial tile forward, tail, partial tile backward */
+    V4 q{0, 0, 0, 0};
+    if (lane == 0) {
+        double *pp = s_part;
+        for (int b = 0; b < Lp; ++b) {
+            double *r = pp + b * NAT_PART;
+            r[12] = S.a; r[13] = S.b; r[14] = S.c; r[15] = S.d;
+            S = add4(mv(Mm, S), V4{r[0], r[1], r[2], r[3]});
+        }
+        auto xt = [&](int64_t k) { return s_tail[k - tlo]; };   /* k in [tlo, n) */
+        const int64_t nt = ntl + 15;                            /* tail length incl. right pad */
+        const double xl = xt(n - 1);
+        {
+            V4 z = S;
+            for (int64_t k = 0; k < nt; ++k) {
+                const int64_t xi = base + k;
+                const double u = xi < n ? xt(xi) : odd_ext(wdt, xl, xt(n - 2 - (xi - n)));
+                s_ytl[k] = SS.step(z, u);
+            }
+        }
+        const double y0 = s_ytl[nt - 1];
+        q = V4{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
+        for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, s_ytl[k]);
+        yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
+        for (int b = Lp - 1; b >= 0; --b) {
+            const double *r = pp + b * NAT_PART;
+            const V4 Sj{r[12], r[13], r[14], r[15]};
+            q = add4(mv(Mm, q), add4(mv(Pm, Sj), V4{r[4], r[5], r[6], r[7]}));
+            yd[Tf * bt + b] = dot4(Cv, q) + Dd * (dot4(Cv, Sj) + Dd * r[8]);
         }
     }
-    const double y0 = tl[nt - 1];
-    V4 q{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
-    for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, tl[k]);
-    yd[nd - 1] = dot4(Cv, q) + Dd * tl[0];
-    for (int b = Lp - 1; b >= 0; --b) {
-        const double *r = pp + b * NAT_PART;
-        const V4 Sj = nat_ld4(r + 12);
-        q = add4(mv(Mm, q), add4(mv(Pm, Sj), nat_ld4(r + 4)));
-        yd[Tf * bt + b] = dot4(Cv, q) + Dd * (dot4(Cv, Sj) + Dd * r[8]);
-    }
-    for (int64_t t = t0 + Tf - 1; t >= t0; --t) {
-        double *c = A.carry + t * 8;
-        c[4] = q.a; c[5] = q.b; c[6] = q.c; c[7] = q.d;
-        q = add4(add4(mv(MT, q), nat_ld4(A.agg + t * 8 + 4)), mv(G0, nat_ld4(c)));
+    /* backward tile carries: car[t][4..7] = Qe_t; Q_start = M^T Qe + R0 + G0 S0 */
+    for (int64_t c1 = Tf; c1 > 0; c1 -= NC_CH) {
+        const int64_t c0 = c1 - NC_CH > 0 ? c1 - NC_CH : 0;
+        const int cn = (int)(c1 - c0);
+        for (int k = lane; k < cn * 8; k += 64) {
+            const int t = k >> 3, j = k & 7;
+            s_in[k] = j < 4 ? car[(c0 + t) * 8 + j] : agg[(c0 + t) * 8 + j];   /* S0_t | R0_t */
+        }
+        __syncthreads();
+        if (lane == 0) {
+            for (int t = cn - 1; t >= 0; --t) {
+                s_out[t * 4 + 0] = q.a; s_out[t * 4 + 1] = q.b; s_out[t * 4 + 2] = q.c; s_out[t * 4 + 3] = q.d;
+                const V4 s0{s_in[t * 8], s_in[t * 8 + 1], s_in[t * 8 + 2], s_in[t * 8 + 3]};
+                const V4 r0{s_in[t * 8 + 4], s_in[t * 8 + 5], s_in[t * 8 + 6], s_in[t * 8 + 7]};
+                q = add4(add4(mv(MT, q), r0), mv(G0, s0));
+            }
+        }
+        __syncthreads();
+        for (int k = lane; k < cn * 4; k += 64) car[(c0 + k / 4) * 8 + 4 + (k & 3)] = s_out[k];
+        __syncthreads();
     }
 }
 
@@ -754,7 +798,6 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     double *agg = (double *)ctx->buf("nat_agg", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
     double *carry = (double *)ctx->buf("nat_carry", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
     double *part = (double *)ctx->buf("nat_part", (size_t)F * 64 * NAT_PART * 8, &rc);
-    double *tail = (double *)ctx->buf("nat_tail", (size_t)F * (ds + 16) * 8, &rc);
     double *yd = O->y ? O->y : (double *)ctx->buf("nat_yd", (size_t)doff[F] * 8, &rc);
     double2 *z = (double2 *)ctx->buf("nat_z", (size_t)doff[F] * 16, &rc);
     double *hb = (double *)ctx->buf("nat_h", (size_t)doff[F] * 8, &rc);
@@ -787,7 +830,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         NatCarryArgs a;
         a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.boff = d_geo; a.toff = d_geo + F + 1;
         a.active = d_active; a.n_files = F; a.dtype = P->dtype; a.channels = P->channels; a.ds = ds; a.bt = bt;
-        a.tab = d_tab; a.tt = d_tt; a.agg = agg; a.part = part; a.carry = carry; a.tail = tail; a.yd = yd;
+        a.tab = d_tab; a.tt = d_tt; a.agg = agg; a.part = part; a.carry = carry; a.yd = yd;
         SosStep ss;
         for (int i = 0; i < 12; ++i) ss.s[i] = P->sos[i];
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
