@@ -346,9 +346,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         double *wm_sorted = use_wm ? (double *)ctx->buf("wm_sorted", (size_t)sumnd * 8, &rc) : nullptr;
         if (rc != BPMX_OK) return rc;
         const size_t wm_lds = wm_lds_bytes(std::min<int64_t>(maxnd, WM_MMAX));
-        auto rollq = [&](const int32_t *run, const int64_t *tr, double *outp, int32_t *allnan) -> int {
+        auto rollq = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, double *outp,
+                         int32_t *allnan) -> int {
             RollqArgs a;
             a.dense = dense; a.doff = d_doff; a.troughs = tr; a.run = run; a.n_files = F;
+            a.env = O->env; a.ntr = ntr;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
             a.out = outp; a.allnan = allnan; a.wm_max = use_wm ? WM_MMAX : 0;
             if (use_wm) {
@@ -374,10 +376,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         {
             InterpArgs a;
             a.env = O->env; a.doff = d_doff; a.troughs = rawt; a.ntr = d_nraw; a.run = d_run1; a.n_files = F;
-            a.dense = dense;
+            a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1;
             LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
         }
-        if ((rc = rollq(d_run1, rawt, draft, d_an1)) != BPMX_OK) return rc;
+        if ((rc = rollq(d_run1, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {
             SanitizeArgs a;
             a.env = O->env; a.draft = draft; a.doff = d_doff; a.active = d_active; a.raw = rawt; a.nraw = d_nraw;
@@ -388,10 +390,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         {
             InterpArgs a;
             a.env = O->env; a.doff = d_doff; a.troughs = O->troughs; a.ntr = O->n_troughs; a.run = d_run2;
-            a.n_files = F; a.dense = dense;
+            a.n_files = F; a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1;
             LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
         }
-        if ((rc = rollq(d_run2, O->troughs, O->floor, d_an2)) != BPMX_OK) return rc;
+        if ((rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2)) != BPMX_OK) return rc;
         {
             FinalArgs a;
             a.draft = draft; a.doff = d_doff; a.active = d_active; a.qv = qv; a.allnan_draft = d_an1;

@@ -85,6 +85,30 @@ __host__ __device__ __forceinline__ double np_lerp(double a, double b, double t)
     return a + d * t;
 }
 
+/* np.interp(x, t, v) with NaN left of t[0] — bpm_analysis.py:1082 /
+ * numpy/_core/src/multiarray/compiled_base.c arr_interp: slope*(x-x0)+y0,
+ * falling back to the right-anchored form (and y0 when y0 == y1) on NaN.
+ * t: m ascending positions, v(j): the value at t[j]. */
+template <typename TP, typename VF>
+__device__ __forceinline__ double interp_at(int64_t x, const TP *t, VF v, int m) {
+    if (m == 0 || x < (int64_t)t[0]) return __builtin_nan("");
+    int lo = 0, hi = m;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)t[mid] <= x) lo = mid + 1; else hi = mid;
+    }
+    const int j = lo - 1;
+    if (j == m - 1 || (int64_t)t[j] == x) return v(j);
+    const double y0 = v(j), y1 = v(j + 1);
+    const double slope = (y1 - y0) / ((double)t[j + 1] - (double)t[j]);
+    double r = slope * ((double)x - (double)t[j]) + y0;
+    if (r != r) {
+        r = slope * ((double)x - (double)t[j + 1]) + y1;
+        if (r != r && y0 == y1) r = y0;
+    }
+    return r;
+}
+
 /* pandas centered fixed window (pandas/core/indexers/objects.py:93-120) */
 __host__ __device__ __forceinline__ void win_bounds(int64_t i, int64_t n, int64_t w, int64_t &s, int64_t &e) {
     int64_t off = (w - 1) / 2;

@@ -80,6 +80,7 @@ struct InterpArgs {
     const int32_t *run;      /* [F] files to process */
     int32_t n_files;
     double *dense;
+    int64_t skip_n;          /* skip files with n <= skip_n and <= WM_TRMAX troughs (k_rollq_wm interpolates) */
 };
 
 struct RollqArgs {
@@ -92,6 +93,8 @@ struct RollqArgs {
     double *out;
     int32_t *allnan;         /* [F] */
     int32_t wm_max;          /* k_rolling_quantile skips files with n <= wm_max (k_rollq_wm took them) */
+    const double *env;       /* k_rollq_wm: interpolate dense from env at the troughs itself ... */
+    const int32_t *ntr;      /* ... when the file has <= WM_TRMAX of them (else read dense) */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -149,14 +152,16 @@ __global__ void k_rolling_quantile(RollqArgs A);
 constexpr int WM_T = 1024;
 constexpr int WM_ITEMS = 18;                 /* 16-bit positions; LDS ~156 KB at the maximum */
 constexpr int WM_MMAX = WM_T * WM_ITEMS;     /* 18432 decimated samples (61 s at 302 Hz) */
+constexpr int WM_TRMAX = 512;                /* troughs staged in LDS for the in-kernel interpolation */
 __host__ __device__ inline size_t wm_lds_bytes(int64_t nmax) {
     const int64_t m = nmax < 1 ? 1 : nmax;
     const int64_t L = m > 1 ? 64 - __builtin_clzll((unsigned long long)(m - 1)) : 1;
     const int64_t NW = (m + 63) / 64;
     const int64_t m8 = (m + 7) & ~7LL;
     const int64_t sort_b = 8 * m8 + (int64_t)(WM_T / 64) * 128 * 4;   /* pos x2, key halves, counters */
+    /* + troughs (WM_TRMAX * 12 B) and their per-64-block index, after the larger phase */
     const int64_t wm_b = 4 * m8 + L * (2 * NW + 1) * 8;               /* sequences x2, levels */
-    return (size_t)(sort_b > wm_b ? sort_b : wm_b);
+    return (size_t)(sort_b > wm_b ? sort_b : wm_b) + (size_t)WM_TRMAX * 12 + (size_t)(m / 64 + 2) * 4;
 }
 __global__ void k_rollq_wm(RollqArgs A, double *sorted_scratch);
 

@@ -3,7 +3,8 @@
  *
  *   k_interp            reindex(arange(Nd)).interpolate() of the trough
  *                       samples == numpy arr_interp (slope*(x-x0)+y0), NaN
- *                       before the first trough.
+ *                       before the first trough (interp_at); only for the
+ *                       recordings k_rollq_wm does not interpolate itself.
  *   k_rolling_quantile  .rolling(W, min_periods=3, center=True).quantile(q)
  *                       .bfill().ffill() — exact order statistics.
  *   k_sanitize          keep trough t iff draft[t] is not NaN and
@@ -37,31 +38,10 @@ __global__ __launch_bounds__(256) void k_interp(InterpArgs A) {
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (x >= n) return;
+    if (n <= A.skip_n && A.ntr[f] <= WM_TRMAX) return;      /* k_rollq_wm interpolates these itself */
     const int64_t *t = A.troughs + d0;
     const double *e = A.env + d0;
-    const int m = A.ntr[f];
-    double r;
-    if (m == 0 || x < t[0]) {
-        r = __builtin_nan("");
-    } else {
-        int lo = 0, hi = m;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (t[mid] <= x) lo = mid + 1; else hi = mid;
-        }
-        const int j = lo - 1;
-        if (j == m - 1 || t[j] == x) {
-            r = e[t[j]];
-        } else {
-            const double y0 = e[t[j]], y1 = e[t[j + 1]];
-            const double slope = (y1 - y0) / ((double)t[j + 1] - (double)t[j]);
-            r = slope * ((double)x - (double)t[j]) + y0;
-            if (r != r) {
-                r = slope * ((double)x - (double)t[j + 1]) + y1;
-                if (r != r && y0 == y1) r = y0;
-            }
-        }
-    }
+    const double r = interp_at(x, t, [&](int j) { return e[t[j]]; }, A.ntr[f]);
     A.dense[d0 + x] = r;
 }
 

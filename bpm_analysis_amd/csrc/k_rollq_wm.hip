@@ -74,6 +74,53 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     if (tid == 0) { s_first = INT_MAX; s_last = -1; }
     STAMP_DECL
 
+    /* dense = np.interp of the troughs (k_interp), evaluated here from env at
+     * the troughs staged in LDS when there are <= WM_TRMAX of them */
+    const int ntr = A.env ? A.ntr[f] : 0;
+    const bool fused = A.env && ntr <= WM_TRMAX;
+    int32_t *s_tp, *s_bj;
+    double *s_tv;
+    {
+        const int64_t n8 = (n + 7) & ~7LL;
+        const int64_t Ln = n > 1 ? 64 - __builtin_clzll((unsigned long long)(n - 1)) : 1;
+        const int64_t sort_b = 8 * n8 + (int64_t)NWV * 128 * 4;
+        const int64_t wm_b = 4 * n8 + Ln * (2 * ((n + 63) / 64) + 1) * 8;
+        s_tv = (double *)(smem + (sort_b > wm_b ? sort_b : wm_b));
+        s_tp = (int32_t *)(s_tv + WM_TRMAX);
+        s_bj = s_tp + WM_TRMAX;                              /* [n/64 + 1]: last trough <= block start */
+    }
+    if (fused) {
+        const int64_t *tr = A.troughs + d0;
+        for (int j = tid; j < ntr; j += WM_T) {
+            s_tp[j] = (int32_t)tr[j];
+            s_tv[j] = A.env[d0 + tr[j]];
+        }
+        __syncthreads();
+        for (int64_t b = tid; b <= (n >> 6); b += WM_T) {
+            int lo = 0, hi = ntr;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= (b << 6)) lo = mid + 1; else hi = mid; }
+            s_bj[b] = lo - 1;
+        }
+        __syncthreads();
+    }
+    /* interp_at's arithmetic, with the bracketing trough found from the block table */
+    auto dval = [&](int64_t x) -> double {
+        if (!fused) return dense[x];
+        if (ntr == 0 || x < s_tp[0]) return __builtin_nan("");
+        int j = s_bj[x >> 6];
+        if (j < 0) j = 0;
+        while (j + 1 < ntr && s_tp[j + 1] <= x) ++j;
+        if (j == ntr - 1 || s_tp[j] == x) return s_tv[j];
+        const double y0 = s_tv[j], y1 = s_tv[j + 1];
+        const double slope = (y1 - y0) / ((double)s_tp[j + 1] - (double)s_tp[j]);
+        double r = slope * ((double)x - (double)s_tp[j]) + y0;
+        if (r != r) {
+            r = slope * ((double)x - (double)s_tp[j + 1]) + y1;
+            if (r != r && y0 == y1) r = y0;
+        }
+        return r;
+    };
+
     /* LDS, sort phase: posA[m8] | posB[m8] | kh[m8] | cnt[NWV][128] (two 16-bit counters per word).
      * Slots >= m are padding: they sort last, so they are neither stored nor counted. */
     const int m8 = (m + 7) & ~7;
@@ -86,7 +133,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     uint64_t kor = 0, kand = ~0ull;
     for (int p = tid; p < m; p += WM_T) {
         posA[p] = (uint16_t)p;                               /* slot order == position order */
-        const uint64_t k = wm_key(dense[t0 + p]);
+        const uint64_t k = wm_key(dval(t0 + p));
         kh[p] = (uint32_t)k;
         kor |= k;
         kand &= k;
@@ -107,7 +154,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     uint32_t *wc = cnt + wid * 128;
     for (int d = 0; d < 8; ++d) {
         if (d == 4 && (vary >> 32)) {                        /* high halves, indexed by position */
-            for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(wm_key(dense[t0 + p]) >> 32);
+            for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(wm_key(dval(t0 + p)) >> 32);
             __syncthreads();
         }
         if (((vary >> (8 * d)) & 0xFFull) == 0) continue;    /* uniform: constant digit, order unchanged */
@@ -194,7 +241,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     WmRec *lv = (WmRec *)kh;                                  /* [L][NR] */
     for (int r = tid; r < m; r += WM_T) {
         const int p = posA[r];
-        sv[r] = dense[t0 + p];
+        sv[r] = dval(t0 + p);
         seqA[p] = (uint16_t)r;
     }
     __syncthreads();

@@ -64,6 +64,7 @@ int main(int argc, char **argv) {
         RollqArgs a;
         a.dense = d_dense; a.doff = d_doff; a.troughs = d_tr; a.run = d_run; a.n_files = F; a.window = W;
         a.min_periods = 3; a.cap = cap; a.q = 0.2; a.out = d_out; a.allnan = d_an; a.stamps = d_st;
+        a.wm_max = 0; a.env = nullptr; a.ntr = nullptr;
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
@@ -100,6 +101,7 @@ int main(int argc, char **argv) {
         RollqArgs a;
         a.dense = d_dense; a.doff = d_doff; a.troughs = d_tr; a.run = d_run; a.n_files = F; a.window = W;
         a.min_periods = 3; a.cap = 0; a.q = 0.2; a.out = d_out; a.allnan = d_an; a.stamps = d_st; a.wm_max = WM_MMAX;
+        a.env = nullptr; a.ntr = nullptr;
         double *d_sorted;
         CK(hipMalloc(&d_sorted, dense.size() * 8));
 
