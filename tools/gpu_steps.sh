@@ -15,7 +15,7 @@ run() {
 }
 for step in "$@"; do
   case $step in
-    pytest) run pytest_gpu 1000 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_ref) run bench_ref 600 python bench.py --steps 10 --warmup 2 --mode reference ;;
