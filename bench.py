@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-files", type=int, default=-1, help="CPU baseline sample size (-1: auto, 0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=3, help="steps of the PCIe-inclusive side measurement (0: skip)")
+    ap.add_argument("--options", type=int, default=0, help="bpmx_option bits (diagnostics; 0 = defaults)")
     return ap.parse_args()
 
 
@@ -174,7 +175,7 @@ def main():
     nd = -(-n // d.ds)
 
     def step():
-        det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d)
+        det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=args.options)
 
     for _ in range(args.warmup):
         step()

@@ -54,6 +54,18 @@ struct NatTile {
     int32_t f, pad;
 };
 
+/* tile headers through the scalar cache (constant address space): a vector
+ * load would wait in vmcnt order behind the in-flight prefetch */
+__device__ __forceinline__ NatTile nat_tile_ld(const NatTile *p, int64_t t) {
+    typedef const __attribute__((address_space(4))) int64_t c64;
+    c64 *q = (c64 *)(p + __builtin_amdgcn_readfirstlane((int)t));   /* t is wave-uniform by contract */
+    NatTile r;
+    r.s0 = q[0]; r.gbase = q[1]; r.ybase = q[2];
+    const int64_t a = q[3], b = q[4];
+    r.j0 = (int32_t)a; r.nb = (int32_t)(a >> 32); r.f = (int32_t)b; r.pad = (int32_t)(b >> 32);
+    return r;
+}
+
 struct NatBlockArgs {
     const void *pcm;
     const NatTile *tiles;
@@ -203,8 +215,23 @@ __device__ __forceinline__ double dot4(const V4 &a, const V4 &b) {
     return __builtin_fma(a.a, b.a, __builtin_fma(a.b, b.b, __builtin_fma(a.c, b.c, a.d * b.d)));
 }
 
-__device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const NatTile &tl, int64_t t, int lane,
-                                                  bool valid, V4 u, V4 v, double x) {
+/* The epilogue's constants, staged in LDS once per workgroup: a vector load
+ * here would sit behind the next tile's prefetch in vmcnt order and stall the
+ * wave until the whole prefetch landed. */
+enum { ET_KPOW = 0, ET_P = 96, ET_C = 112, ET_D = 116, ET_SIZE = 117 };
+__device__ __forceinline__ void nat_stage_epilogue_tables(const NatBlockArgs &A, double *et) {
+    for (int i = threadIdx.x; i < ET_SIZE; i += blockDim.x) {
+        double v;
+        if (i < ET_P) v = A.tt[TT_KPOW + i];
+        else if (i < ET_C) v = A.tab[TB_P + i - ET_P];
+        else if (i < ET_D) v = A.tab[TB_C + i - ET_C];
+        else v = A.tab[TB_D];
+        et[i] = v;
+    }
+}
+
+__device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const double *et, const NatTile &tl,
+                                                  int64_t t, int lane, bool valid, V4 u, V4 v, double x) {
     const int bt = A.bt;
     const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
     if (Lt < bt) {                                        /* partial last tile: raw blocks */
@@ -216,8 +243,6 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const N
         }
         return;
     }
-    const double *__restrict__ tb = A.tab;
-    const double *__restrict__ tt = A.tt;
     if (!valid) { u = V4{0, 0, 0, 0}; v = V4{0, 0, 0, 0}; x = 0; }
     /* incl_b = sum_{c<=b} M^(b-c) u_c */
     V4 incl = u;
@@ -225,20 +250,20 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const N
     for (int k = 0; k < 6; ++k) {
         const int d = 1 << k;
         const V4 y = shfl_up_v(incl, d);
-        if (lane >= d) incl = add4(incl, mv(nat_ld16(tt + TT_KPOW + 16 * k), y));
+        if (lane >= d) incl = add4(incl, mv(nat_ld16(et + ET_KPOW + 16 * k), y));
     }
     V4 loc = shfl_up_v(incl, 1);
     if (lane == 0) loc = V4{0, 0, 0, 0};
     /* R_b = sum_{c>=b} M^(c-b) (P loc_c + v_c) */
-    V4 R = valid ? add4(mv(nat_ld16(tb + TB_P), loc), v) : V4{0, 0, 0, 0};
+    V4 R = valid ? add4(mv(nat_ld16(et + ET_P), loc), v) : V4{0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const int d = 1 << k;
         const V4 y = shfl_down_v(R, d);
-        if (lane + d < 64) R = add4(R, mv(nat_ld16(tt + TT_KPOW + 16 * k), y));
+        if (lane + d < 64) R = add4(R, mv(nat_ld16(et + ET_KPOW + 16 * k), y));
     }
-    const V4 C = nat_ld4(tb + TB_C);
-    const double D = tb[TB_D];
+    const V4 C = nat_ld4(et + ET_C);
+    const double D = et[ET_D];
     if (valid) A.gam[tl.gbase + lane] = dot4(C, R) + D * dot4(C, loc) + D * D * x;
     double *ag = A.agg + t * 8;
     if (lane == bt - 1) { ag[0] = incl.a; ag[1] = incl.b; ag[2] = incl.c; ag[3] = incl.d; }
@@ -264,13 +289,15 @@ typedef uint32_t nat_u4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const double *__restrict__ coef) {
     typedef nat_u4 u4;
     __shared__ u4 tile[NB_RCH * 64];
+    __shared__ double s_et[ET_SIZE];
+    nat_stage_epilogue_tables(A, s_et);
     const int lane = threadIdx.x;
     const int16_t *pcm = (const int16_t *)A.pcm;
     const int64_t total = A.total;
     const int ds = A.ds, bt = A.bt;
     const int nch = (7 + bt * ds + 1 + 7) >> 3;           /* chunks a tile may touch */
     auto issue = [&](int64_t t, u4 *reg, int &off) {
-        const int64_t s0 = A.tiles[t].s0;
+        const int64_t s0 = nat_tile_ld(A.tiles, t).s0;
         const int64_t a0 = s0 & ~(int64_t)7;
         off = (int)(s0 - a0);
 #pragma unroll
@@ -286,7 +313,7 @@ __global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const 
     int64_t t = blockIdx.x;
     if (t < A.n_tiles) issue(t, reg, off);
     while (t < A.n_tiles) {
-        const NatTile tl = A.tiles[t];
+        const NatTile tl = nat_tile_ld(A.tiles, t);
 #pragma unroll
         for (int r = 0; r < NB_RCH; ++r) tile[r * 64 + lane] = reg[r];
         const int coff = off;
@@ -330,7 +357,7 @@ __global__ __launch_bounds__(64) void k_native_blocks_i16(NatBlockArgs A, const 
             for (; i < L; ++i) acc((double)th[base + i], coef + (int64_t)i * 8);
             x0 = (double)th[base];
         }
-        nat_tile_epilogue(A, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+        nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
         __syncthreads();
         t = tn;
     }
@@ -342,7 +369,10 @@ template <int DT, bool MULTI>
 __global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
     const int64_t t = blockIdx.x;
     if (t >= A.n_tiles) return;
-    const NatTile tl = A.tiles[t];
+    __shared__ double s_et[ET_SIZE];
+    nat_stage_epilogue_tables(A, s_et);
+    __syncthreads();
+    const NatTile tl = nat_tile_ld(A.tiles, t);
     const int lane = threadIdx.x, ds = A.ds;
     const int j = tl.j0 + lane;
     const bool valid = lane < A.bt && j < tl.nb;
@@ -360,8 +390,186 @@ __global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
             if (i == 0) x0 = xv;
         }
     }
-    nat_tile_epilogue(A, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+    nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
 }
+
+/* ---------------------------------------------------------------------- */
+/* int16 mono, exact-integer path on the matrix cores.
+ *
+ * The 8 block projections are a GEMM: [64 blocks x K samples] x [K x 8
+ * coefficients], K = ds + 1 padded to 32 * KS.  The f64 VALU form above is
+ * bound by 8 f64 FMAs per sample (~2x the HBM time of reading the PCM), so the
+ * coefficients are quantised instead: q_c,i = round(coef_c,i * 2^(P - e_c))
+ * with 2^e_c >= max_i |coef_c,i| (|q| <= 2^54, i.e. 2^-55 of the column's
+ * largest coefficient — below f64 rounding of the coefficient itself) and
+ * split into 7 balanced base-256 digits d_r.  A sample splits exactly into
+ * x = 256 h + (l - 128) + 128 with h = x >> 8 and l - 128 = (x & 255) ^ 0x80,
+ * both int8, so
+ *     sum_i q_i x_i = sum_r 256^r [ sum_i d_r,i (l_i - 128) + sum_i d_(r-1),i h_i ] + 128 sum_i q_i
+ * and each bracket is one int32 accumulator row of v_mfma_i32_32x32x32_i8
+ * (the 128 sum q term enters as the accumulators' initial value, digit by
+ * digit).  8 digit rows x 8 coefficients = two 32-row M tiles; per 32-block N
+ * tile and K step four MFMAs.  Every sum is exact in int32; the 8 rows
+ * combine exactly into two int64 halves, and the only rounding is the final
+ * conversion to f64 (then an exact power-of-two scale).
+ *
+ * Fragment maps (32x32x32 i8): A lane l = row (l & 31) x 16 consecutive k of
+ * k-group l >> 5, B likewise with column (l & 31); the same (lane half, byte)
+ * -> k map on both operands makes the product the sum over the K step.
+ * Accumulator: lane l = column (block) l & 31, register 4q + i = row
+ * 8q + 4(l >> 5) + i, which the tables assign to coefficient 2q + (l >> 5),
+ * digit row 4t + i (t = M tile): each lane ends with every digit row of 4
+ * coefficients of its block, and one lane-half exchange gives lane b all 8
+ * of block b. */
+typedef int32_t nm_i4 __attribute__((ext_vector_type(4)));
+typedef int32_t nm_i16 __attribute__((ext_vector_type(16)));
+
+/* Feeding it: a tile is 64 blocks (~18.7 KB of PCM).  With a tile per wave
+ * in flight the chip sits at ~5 TB/s, so tiles travel HBM -> LDS directly by
+ * LDS-DMA (global_load_lds_dwordx4, no registers), two slots per wave: the
+ * DMA of tile k+2 is issued as soon as the matrix phase of tile k has read its
+ * slot, and flies during tile k's epilogue and tile k+1's matrix phase.  Four
+ * waves per workgroup, one workgroup per CU: 8 slots + the shared tables fill
+ * the 160 KiB LDS. */
+constexpr int NM_WAVES = 4;
+constexpr int NM_SLOTS = 1;                       /* LDS tile slots per wave */
+constexpr int NM_MINW = 2;                        /* waves per SIMD the register budget must allow */
+constexpr int NM_NDMA = 18;                      /* DMA wave-instructions per tile, always all issued, all lanes on */
+constexpr int NM_SLOT_CH = NM_NDMA * 64;          /* 16-byte chunks per slot (18,432 B) */
+
+/* blocks per tile the slot holds: every k of the last block's K steps (+2
+ * samples for the odd-offset align) must stay inside the slot */
+__host__ __device__ constexpr int nm_tile_blocks(int ds, int ks) {
+    return ((NM_SLOT_CH * 8 - 7 - 32 * ks - 2) / ds + 1) < 64 ? ((NM_SLOT_CH * 8 - 7 - 32 * ks - 2) / ds + 1) : 64;
+}
+
+template <int KS>
+__global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(NatBlockArgs A, const nm_i4 *__restrict__ afrag,
+                                                                      const nm_i16 *__restrict__ ainit,
+                                                                      const double *__restrict__ cscale) {
+    typedef nat_u4 u4;
+    __shared__ u4 slots[NM_WAVES * NM_SLOTS][NM_SLOT_CH];
+    __shared__ double s_et[ET_SIZE];
+    __shared__ nm_i16 s_init[4];                        /* accumulator start values [M tile][lane half] */
+    nat_stage_epilogue_tables(A, s_et);
+    for (int i = threadIdx.x; i < 4; i += blockDim.x) s_init[i] = ainit[(i >> 1) * 64 + (i & 1) * 32];
+    /* wave-uniform (readfirstlane): tile headers must come through the scalar cache */
+    const int lane = lane_id(), hf = lane >> 5, wv = __builtin_amdgcn_readfirstlane(wave_id());
+    const int16_t *pcm = (const int16_t *)A.pcm;
+    const int64_t total = A.total;
+    const int ds = A.ds, bt = A.bt;
+    const int nch = (7 + bt * ds + 1 + 7) >> 3;          /* <= NM_SLOT_CH (host: nm_tile_blocks) */
+    nm_i4 af[2][KS][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) af[t][s][v] = afrag[((t * KS + s) * 2 + v) * 64 + lane];
+    double sc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sc[q] = cscale[2 * q + hf];
+    __syncthreads();                                      /* s_et, s_init */
+
+    /* chunk q of a tile -> slot chunk q (lane l of DMA r moves chunk 64r + l) */
+    /* Exactly NM_NDMA instructions per tile with every lane on (the vmcnt
+     * arithmetic below depends on it): chunks past the tile or the batch
+     * re-read the batch's last whole chunk into the slot's spare room. */
+    const int64_t clast = (total & ~(int64_t)7) - 8;
+    auto dma = [&](int64_t t, u4 *slot) {
+        const int64_t a0 = nat_tile_ld(A.tiles, t).s0 & ~(int64_t)7;
+#pragma unroll
+        for (int r = 0; r < NM_NDMA; ++r) {
+            const int q = r * 64 + lane;
+            int64_t c = a0 + (int64_t)q * 8;
+            c = (q < nch && c + 8 <= total) ? c : clast;
+            /* inline asm, not __builtin_amdgcn_global_load_lds: the compiler cannot
+             * tell the slots apart and would put a vmcnt(0) before the next LDS
+             * read, draining the other slot's DMA too.  The waits are explicit
+             * (vmcnt below); a compiler-generated wait can only over-wait. */
+            const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(slot + r * 64);
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                         :: "v"(pcm + c), "s"(m0) : "memory");
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * NM_WAVES;
+    int64_t t = (int64_t)blockIdx.x * NM_WAVES + wv;
+    if (t < A.n_tiles) dma(t, slots[NM_SLOTS * wv]);
+    if (NM_SLOTS == 2 && t + stride < A.n_tiles) dma(t + stride, slots[NM_SLOTS * wv + 1]);
+    for (int k = 0; t < A.n_tiles; ++k, t += stride) {
+        u4 *slot = slots[NM_SLOTS * wv + (NM_SLOTS == 2 ? (k & 1) : 0)];
+        /* Issued after this tile's DMA: the next tile's NM_NDMA (when there is
+         * a next tile) and a few epilogue stores.  vmcnt retires in issue
+         * order, so <= NM_NDMA outstanding covers this tile (over-waiting by
+         * at most the stores' count of the next tile's chunks); with no next
+         * tile, wait for everything. */
+        if (NM_SLOTS == 2 && t + stride < A.n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NM_NDMA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const NatTile tl = nat_tile_ld(A.tiles, t);
+        const int coff = (int)(tl.s0 & 7);
+        {
+            const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
+            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))   /* last tile of the batch */
+                ((int16_t *)slot)[tail0 - a0 + lane] = pcm[tail0 + lane];
+        }
+        const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
+        const uint32_t *tw = (const uint32_t *)slot;
+        double res[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const int b = 32 * n + (lane & 31);
+            const int hw0 = coff + (b < Lt ? b : 0) * ds + 16 * hf;      /* halfword index of k-group start */
+            const uint32_t sh = (hw0 & 1) ? 16u : 0u;
+            nm_i16 acc0 = s_init[hf], acc1 = s_init[2 + hf];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const uint32_t *p = tw + ((hw0 + 32 * s) >> 1);
+                uint32_t w[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) w[i] = p[i];
+                nm_i4 bh, bl;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t e0 = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sh);
+                    const uint32_t e1 = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sh);
+                    bh[i] = (int32_t)__builtin_amdgcn_perm(e1, e0, 0x07050301u);
+                    bl[i] = (int32_t)(__builtin_amdgcn_perm(e1, e0, 0x06040200u) ^ 0x80808080u);
+                }
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s][0], bl, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s][0], bl, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s][1], bh, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s][1], bh, acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t lo = (int64_t)acc0[4 * q] + ((int64_t)acc0[4 * q + 1] << 8) +
+                                   ((int64_t)acc0[4 * q + 2] << 16) + ((int64_t)acc0[4 * q + 3] << 24);
+                const int64_t hi = (int64_t)acc1[4 * q] + ((int64_t)acc1[4 * q + 1] << 8) +
+                                   ((int64_t)acc1[4 * q + 2] << 16) + ((int64_t)acc1[4 * q + 3] << 24);
+                res[n][q] = ((double)hi * 4294967296.0 + (double)lo) * sc[q];   /* |hi|, |lo| < 2^53: exact */
+            }
+        }
+        const int j = tl.j0 + lane;
+        const bool valid = lane < bt && j < tl.nb;
+        const double x0 = valid ? (double)((const int16_t *)slot)[coff + lane * ds] : 0.0;
+        /* the slot is read: refill it with the tile after next (two slots) or
+         * the next one (one slot: it flies during this epilogue) */
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (t + NM_SLOTS * stride < A.n_tiles) dma(t + NM_SLOTS * stride, slot);
+        /* lane half 0 holds even coefficients, half 1 odd ones; N tile n = blocks 32n.. */
+        double cf[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double other = __shfl_xor(hf ? res[0][q] : res[1][q], 32);
+            cf[2 * q] = hf ? other : res[0][q];
+            cf[2 * q + 1] = hf ? res[1][q] : other;
+        }
+        nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{cf[0], cf[1], cf[2], cf[3]}, V4{cf[4], cf[5], cf[6], cf[7]},
+                          x0);
+    }
+}
+template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
+template __global__ void k_native_blocks_mfma<5>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 
 /* One wave per recording (lane 0 carries the sequential recursions):
  *   head  15 padded samples, exact sosfilt steps -> S at block 0;
@@ -488,7 +696,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
 /* yd_j = alpha_b . Qe_t + beta_b . S0_t + gamma_j over full tiles (lane = block) */
 __global__ __launch_bounds__(64) void k_native_yd(NatYdArgs A) {
     const int64_t t = blockIdx.x;
-    const NatTile tl = A.tiles[t];
+    const NatTile tl = nat_tile_ld(A.tiles, t);
     const int bt = A.bt, lane = threadIdx.x;
     if (tl.nb - tl.j0 < bt || lane >= bt) return;          /* partial tiles: k_native_carry */
     const double *c = A.carry + t * 8;
@@ -620,7 +828,7 @@ void lm_vec(const LM &X, const LD *v, LD *out) {
     }
 }
 
-std::vector<double> build_tables(const double *sos, const double *sos_zi, int L, int T) {
+std::vector<double> build_tables(const double *sos, const double *sos_zi, int L, int T, std::vector<LD> *coefld) {
     /* probe the cascade step: s' = A s + B u, y = C s + D u */
     auto step = [&](const LD *z, LD u, LD *zo) -> LD {
         const LD *a = nullptr; (void)a;
@@ -685,6 +893,12 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L,
         for (int i = ip + 1; i <= L; ++i)
             for (int k = 0; k < 4; ++k) g[k] += AB[(size_t)(i - 1) * 4 + k] * h[i - 1 - ip];
         for (int k = 0; k < 4; ++k) c[4 + k] = (double)g[k];
+        if (coefld) {
+            LD *cl = &(*coefld)[(size_t)ip * 8];
+            if (ip < L) lm_vec(pw[L - 1 - ip], Bv, cl);
+            else cl[0] = cl[1] = cl[2] = cl[3] = 0;
+            for (int k = 0; k < 4; ++k) cl[4 + k] = g[k];
+        }
     }
     /* tile tables (native_tables.tile_tables): M^(2^k), M^T, G_0, alpha_b, beta_b */
     {
@@ -725,6 +939,62 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L,
     }
     return out;
 }
+
+/* int8-MFMA tables for k_native_blocks_mfma (layout in 32-bit words):
+ *   [0, 16)                 scale_c = 2^(e_c - P), 8 doubles
+ *   [16, 16 + 2*64*16)      initial accumulators [M tile][lane][16]: 128 * sum_k d_r(k, c)
+ *   then                    A fragments [M tile][K step][variant][lane][4 words]
+ * from the long-double coefficients (R = ds + 1 rows x 8). */
+constexpr int NM_P = 54, NM_D = 7;
+std::vector<int32_t> build_mfma(const std::vector<LD> &cl, int R, int KS) {
+    std::vector<int64_t> q((size_t)R * 8);
+    std::vector<double> scale(8);
+    for (int c = 0; c < 8; ++c) {
+        LD mx = 0;
+        for (int i = 0; i < R; ++i) mx = std::max(mx, fabsl(cl[(size_t)i * 8 + c]));
+        int e = 0;
+        if (mx > 0) frexpl(mx, &e);                          /* mx < 2^e */
+        scale[c] = ldexp(1.0, e - NM_P);
+        for (int i = 0; i < R; ++i) q[(size_t)i * 8 + c] = llroundl(ldexpl(cl[(size_t)i * 8 + c], NM_P - e));
+    }
+    /* balanced base-256 digits, d[(k * 8 + c) * 8 + r], r < NM_D (row 7 stays 0) */
+    std::vector<int8_t> d((size_t)R * 64, 0);
+    for (int i = 0; i < R * 8; ++i) {
+        int64_t v = q[i];
+        for (int r = 0; r < NM_D; ++r) {
+            int dg = (int)(v & 255);
+            if (dg >= 128) dg -= 256;
+            d[(size_t)i * 8 + r] = (int8_t)dg;
+            v = (v - dg) >> 8;
+        }
+    }
+    auto dig = [&](int k, int c, int r) -> int { return (k < R && r >= 0 && r < 8) ? d[((size_t)k * 8 + c) * 8 + r] : 0; };
+    std::vector<int32_t> w(16 + 2 * 64 * 16 + (size_t)2 * KS * 2 * 64 * 4, 0);
+    std::memcpy(w.data(), scale.data(), 64);
+    int32_t *init = w.data() + 16;
+    for (int t = 0; t < 2; ++t)
+        for (int l = 0; l < 64; ++l)
+            for (int reg = 0; reg < 16; ++reg) {
+                const int c = 2 * (reg >> 2) + (l >> 5), r = 4 * t + (reg & 3);
+                int64_t sum = 0;
+                for (int k = 0; k < R; ++k) sum += dig(k, c, r);
+                init[(t * 64 + l) * 16 + reg] = (int32_t)(128 * sum);
+            }
+    int32_t *af = init + 2 * 64 * 16;
+    for (int t = 0; t < 2; ++t)
+        for (int st = 0; st < KS; ++st)
+            for (int v = 0; v < 2; ++v)
+                for (int l = 0; l < 64; ++l) {
+                    const int rho = l & 31;
+                    const int c = 2 * (rho >> 3) + ((rho >> 2) & 1), r = 4 * t + (rho & 3) - v;
+                    for (int j = 0; j < 16; ++j) {
+                        const int k = 32 * st + 16 * (l >> 5) + j;
+                        const uint32_t byte = (uint8_t)(int8_t)dig(k, c, r);
+                        af[(((t * KS + st) * 2 + v) * 64 + l) * 4 + j / 4] |= (int32_t)(byte << (8 * (j & 3)));
+                    }
+                }
+    return w;
+}
 }  // namespace
 
 int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
@@ -737,15 +1007,28 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* tables and block offsets: rebuilt / re-uploaded only when they change (the
      * host copies live in the context, so the async upload never outlives them) */
     /* tiles of bt blocks: the int16 path's LDS tile holds <= NB_RCH*512 samples */
-    const int bt = std::min(64, (NB_RCH * 512 - 16) / ds);
+    /* matrix-core path: int16 mono, ds + 1 <= 160 (KS K steps of 32 samples) */
+    const int mfma_ks = ds + 1 <= 96 ? 3 : (ds + 1 <= 160 ? 5 : 0);
+    const bool use_mfma = mfma_ks && P->dtype == BPMX_DT_I16 && P->channels == 1 && ((uintptr_t)B->pcm & 15) == 0 &&
+                          foff[F] >= 16 && !(P->options & BPMX_OPT_NATIVE_F64);
+    /* tiles of bt blocks: the LDS tile (slot) must hold the tile's samples */
+    const int bt = use_mfma ? nm_tile_blocks(ds, mfma_ks) : std::min(64, (NB_RCH * 512 - 16) / ds);
     std::vector<int64_t> key(16);
     for (int i = 0; i < 12; ++i) std::memcpy(&key[i], &P->sos[i], 8);
     key[12] = ds;
     std::memcpy(&key[13], &P->sos_zi[0], 8);
     std::memcpy(&key[14], &P->sos_zi[2], 8);
     key[15] = bt;
+    size_t mfma_off = 0;                                     /* in doubles, into nat_tab */
     if (key != ctx->nat_key) {
-        ctx->nat_tab = build_tables(P->sos, P->sos_zi, ds, bt);
+        std::vector<LD> cl((size_t)(ds + 1) * 8);
+        ctx->nat_tab = build_tables(P->sos, P->sos_zi, ds, bt, &cl);
+        if (mfma_ks) {
+            const std::vector<int32_t> w = build_mfma(cl, ds + 1, mfma_ks);
+            const size_t o = ctx->nat_tab.size();
+            ctx->nat_tab.resize(o + w.size() / 2);
+            std::memcpy(ctx->nat_tab.data() + o, w.data(), w.size() * 4);
+        }
         ctx->nat_key = key;
         ctx->nat_tab_dirty = true;
     }
@@ -758,6 +1041,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         ctx->nat_tab_dirty = false;
     }
     const double *d_tt = d_tab + TB_COEF + 8 * (size_t)(ds + 1);
+    mfma_off = TB_COEF + 8 * (size_t)(ds + 1) + TT_SIZE;
     /* geometry: block offsets, per-file tile offsets, the tile list (cached with the context) */
     std::vector<int64_t> tk(4 + 2 * (F + 1));
     tk[0] = bt; tk[1] = F; tk[2] = ds; tk[3] = 0;
@@ -807,8 +1091,20 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.pcm = B->pcm; a.tiles = d_tiles; a.n_tiles = nt; a.total = foff[F]; a.bt = bt;
         a.channels = P->channels; a.ds = ds; a.tab = d_tab; a.tt = d_tt; a.gam = gam; a.agg = agg; a.part = part;
         const bool fast = P->dtype == BPMX_DT_I16 && P->channels == 1 && ((uintptr_t)B->pcm & 15) == 0;
-        if (fast) {
-            const unsigned grid = (unsigned)std::min<int64_t>(nt, 256 * 8);
+        const unsigned grid = (unsigned)std::min<int64_t>(nt, 256 * 8);
+        if (use_mfma) {
+            const double *mt = d_tab + mfma_off;
+            const nm_i16 *init = (const nm_i16 *)(mt + 8);
+            const nm_i4 *af = (const nm_i4 *)(mt + 8 + 2 * 64 * 16 / 2);
+            /* persistent: one 4-wave workgroup per CU (LDS-bound) */
+            const unsigned g1 = (unsigned)std::min<int64_t>((nt + NM_WAVES - 1) / NM_WAVES, 256 * (2 / NM_SLOTS));
+            if (mfma_ks == 3)
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma<3>, dim3(g1), dim3(64 * NM_WAVES), 0, s, a, af,
+                       init, mt);
+            else
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma<5>, dim3(g1), dim3(64 * NM_WAVES), 0, s, a, af,
+                       init, mt);
+        } else if (fast) {
             LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16, dim3(grid), dim3(64), 0, s, a,
                    (const double *)(d_tab + TB_COEF));
         } else {

@@ -202,3 +202,31 @@ def test_rolling_quantile_kernels_agree(det, name):
     for opt in (0, N.OPT_ROLLQ_MERGE):
         r = det.run_host([g["pcm"]], int(g["fs"]), g["params"], mode="reference", options=opt)[0]
         _check_file(r, g)
+
+
+@pytest.mark.parametrize("fs", [44100, 22050, 48000])
+def test_native_block_kernels_agree(det, fs):
+    """The exact-integer matrix-core block projections (default for int16 mono,
+    ds + 1 <= 160) are at least as close to the oracle's sosfiltfilt as the f64
+    VALU kernel (BPMX_OPT_NATIVE_F64), and both give the oracle's indices."""
+    import torch
+    from bpm_analysis_amd import _native as N
+    lens = [fs * 9 + 77, fs * 6, fs * 4 + 3]
+    recs = [O.synth(900 + i, n, fs, 1) for i, n in enumerate(lens)]
+    dev = torch.from_numpy(np.concatenate(recs)).to(det.device)
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    outs = []
+    for opt in (0, N.OPT_NATIVE_F64):
+        res = det.run(dev, fo, fs, params, mode="native", want_y=True, options=opt)
+        torch.cuda.synchronize()
+        outs.append(res.to_host())
+    for a, b, pcm in zip(outs[0], outs[1], recs):
+        o = O.detect(pcm, fs, params, mode="native")
+        scale = np.max(np.abs(o["y"]))
+        ea, eb = np.max(np.abs(a["y"] - o["y"])), np.max(np.abs(b["y"] - o["y"]))
+        print(f"fs={fs} n={len(pcm)}: |y_mfma - y_oracle| = {ea / scale:.3e}, |y_f64 - y_oracle| = {eb / scale:.3e} (rel)")
+        assert ea <= max(2 * eb, 1e-12 * scale)
+        assert ea <= 1e-9 * scale
+        _check_file(a, o, exact_env=False)
+        _check_file(b, o, exact_env=False)
