@@ -1,0 +1,42 @@
+/*
+ * bpmx_hilbert.h — fused in-LDS Hilbert magnitude + rolling mean (k_hilbert.hip).
+ */
+#ifndef BPMX_HILBERT_H
+#define BPMX_HILBERT_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace bpmx {
+
+constexpr int HB_T = 1024;                 /* threads per recording */
+constexpr int HB_MAXT = 6;                 /* register-held butterfly outputs per thread per stage */
+constexpr int HB_MAXS = 16;                /* radix stages */
+constexpr int HB_PMAX = 401;               /* largest prime radix (direct DFT cost ~ M p / 2 FMA per stage) */
+constexpr size_t HB_LDS_MAX = 160 * 1024;  /* one workgroup per CU */
+
+struct HilbPlan {
+    int32_t M, N, ns, ntwh, nptab, window;
+    int32_t rad[HB_MAXS], B[HB_MAXS], L[HB_MAXS], ptab[HB_MAXS];
+};
+
+struct HilbArgs {
+    const double *yd;              /* [sumNd] decimated filtered signal */
+    const int64_t *doff;
+    const int32_t *active;
+    int32_t f_begin, f_end;        /* a run of recordings with this plan's Nd */
+    const double2 *tabs;           /* twiddle hi [ntwh] | lo [128] | prime cos/sin tables */
+    double *env;
+};
+
+__global__ void k_hilbert_env(HilbArgs A, HilbPlan P);
+
+/* 1 and the plan, its tables and LDS size when Nd takes the fused kernel; 0 otherwise */
+int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes);
+
+}  // namespace bpmx
+
+#endif

@@ -36,6 +36,7 @@
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 #include "bpmx_native.h"
+#include "bpmx_hilbert.h"
 
 namespace bpmx {
 
@@ -102,6 +103,7 @@ struct NatEnvArgs {
     const int32_t *active;
     int32_t n_files, window;
     double *env;
+    const int32_t *skip;           /* [F] 1: envelope already written by k_hilbert_env */
 };
 
 /* ---------------------------------------------------------------------- */
@@ -540,13 +542,16 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
                 acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s][1], bh, acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s][1], bh, acc1, 0, 0, 0);
             }
+            /* |acc| <= 2*160*128*128 + 128*147*128 < 2^23, so a row pair
+             * a_r + 256 a_(r+1) fits int32; two pairs combine exactly in f64
+             * (< 2^48), and H 2^32 + L is the one rounding. */
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int64_t lo = (int64_t)acc0[4 * q] + ((int64_t)acc0[4 * q + 1] << 8) +
-                                   ((int64_t)acc0[4 * q + 2] << 16) + ((int64_t)acc0[4 * q + 3] << 24);
-                const int64_t hi = (int64_t)acc1[4 * q] + ((int64_t)acc1[4 * q + 1] << 8) +
-                                   ((int64_t)acc1[4 * q + 2] << 16) + ((int64_t)acc1[4 * q + 3] << 24);
-                res[n][q] = ((double)hi * 4294967296.0 + (double)lo) * sc[q];   /* |hi|, |lo| < 2^53: exact */
+                const int32_t p01 = acc0[4 * q] + acc0[4 * q + 1] * 256, p23 = acc0[4 * q + 2] + acc0[4 * q + 3] * 256;
+                const int32_t p45 = acc1[4 * q] + acc1[4 * q + 1] * 256, p67 = acc1[4 * q + 2] + acc1[4 * q + 3] * 256;
+                const double L = __builtin_fma((double)p23, 65536.0, (double)p01);
+                const double H = __builtin_fma((double)p67, 65536.0, (double)p45);
+                res[n][q] = __builtin_fma(H, 4294967296.0, L) * sc[q];
             }
         }
         const int j = tl.j0 + lane;
@@ -728,7 +733,7 @@ constexpr int NE_T = 256;
 __global__ __launch_bounds__(NE_T) void k_native_env(NatEnvArgs A) {
     __shared__ double mag[NE_T + 2 * 1024];
     const int f = blockIdx.y;
-    if (f >= A.n_files || !A.active[f]) return;
+    if (f >= A.n_files || !A.active[f] || A.skip[f]) return;
     const int64_t n = A.doff[f + 1] - A.doff[f];
     const int64_t i0 = (int64_t)blockIdx.x * NE_T;
     if (i0 >= n) return;
@@ -997,6 +1002,42 @@ std::vector<int32_t> build_mfma(const std::vector<LD> &cl, int R, int KS) {
 }
 }  // namespace
 
+/* fused-Hilbert plans and their device tables, cached per (device, Nd, window) */
+struct HbTables {
+    HilbPlan plan;
+    size_t lds = 0;
+    double2 *dev = nullptr;
+};
+std::map<std::tuple<int, int64_t, int>, HbTables> g_hb;
+
+HbTables *hb_tables(bpmx_ctx *ctx, int64_t nd, int window, HilbPlan *P, size_t *lds, hipStream_t s, int *rc) {
+    const auto key = std::make_tuple(ctx->device, nd, window);
+    auto it = g_hb.find(key);
+    if (it == g_hb.end()) {
+        HbTables t;
+        std::vector<double2> tabs;
+        if (!hilbert_plan(nd, window, &t.plan, &tabs, &t.lds)) {
+            t.dev = nullptr;                                   /* remembered: not supported */
+        } else {
+            if (hipMalloc((void **)&t.dev, tabs.size() * sizeof(double2)) != hipSuccess) {
+                *rc = fail(BPMX_E_HIP, "hipMalloc (Hilbert tables) failed");
+                return nullptr;
+            }
+            /* synchronous: the host vector dies here, and this happens once per Nd */
+            if (hipMemcpy(t.dev, tabs.data(), tabs.size() * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess) {
+                *rc = fail(BPMX_E_HIP, "hipMemcpy (Hilbert tables) failed");
+                return nullptr;
+            }
+        }
+        it = g_hb.emplace(key, t).first;
+    }
+    (void)s;
+    if (!it->second.dev) return nullptr;
+    *P = it->second.plan;
+    *lds = it->second.lds;
+    return &it->second;
+}
+
 int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
                     const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active) {
@@ -1136,13 +1177,42 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.tiles = d_tiles; a.bt = bt; a.tt = d_tt; a.carry = carry; a.gam = gam; a.yd = yd;
         LAUNCH(ctx, s, "k_native_yd", k_native_yd, dim3((unsigned)nt), dim3(64), 0, s, a);
     }
-    /* Hilbert: runs of equal Nd share one batched plan */
+    /* Hilbert + envelope: runs of equal Nd share a plan.  The fused LDS kernel
+     * (k_hilbert.hip) takes every run whose Nd factors into small primes and
+     * fits; the rest go through rocFFT + k_hilbert_rotate + k_native_env. */
+    if (P->env_window > 2 * 1024) return fail(BPMX_E_LIMIT, "envelope window too large for k_native_env");
+    bool need_env = false;
+    std::vector<int32_t> &fused = ctx->nat_fused;
+    fused.assign(F, 0);
     int f0 = 0;
     while (f0 < F) {
         const int64_t nd = doff[f0 + 1] - doff[f0];
         int f1 = f0 + 1;
         while (f1 < F && doff[f1 + 1] - doff[f1] == nd) ++f1;
+        HilbPlan hp;
+        size_t hlds = 0;
+        HbTables *ht = nullptr;
+        if (nd > 15 && (doff[f0] & 1) == 0 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) &&
+            (ht = hb_tables(ctx, nd, P->env_window, &hp, &hlds, s, &rc)) != nullptr) {
+            if (rc != BPMX_OK) return rc;
+            /* recordings of the run all start at even offsets? (double2 loads) */
+            bool even = true;
+            for (int f = f0; f < f1; ++f) even = even && (doff[f] & 1) == 0;
+            if (even) {
+                HilbArgs a;
+                a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
+                a.tabs = ht->dev; a.env = O->env;
+                (void)hipFuncSetAttribute((const void *)k_hilbert_env, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)hlds);
+                LAUNCH(ctx, s, "k_hilbert_env", k_hilbert_env, dim3((unsigned)(f1 - f0)), dim3(HB_T), hlds, s, a, hp);
+                for (int f = f0; f < f1; ++f) fused[f] = 1;
+                f0 = f1;
+                continue;
+            }
+        }
+        if (rc != BPMX_OK) return rc;
         if (nd > 15) {
+            need_env = true;
             FftPlans *pl = nullptr;
             if ((rc = get_plans(ctx->device, nd, f1 - f0, &pl)) != BPMX_OK) return rc;
             void *work = pl->work ? ctx->buf("nat_fft_work", pl->work, &rc) : nullptr;
@@ -1172,11 +1242,13 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         }
         f0 = f1;
     }
-    {
-        if (P->env_window > 2 * 1024) return fail(BPMX_E_LIMIT, "envelope window too large for k_native_env");
+    if (need_env) {                                   /* the rocFFT runs (fused runs are skipped) */
+        int32_t *d_fused = (int32_t *)ctx->buf("nat_fused", (size_t)F * 4, &rc);
+        if (rc != BPMX_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(d_fused, fused.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
         NatEnvArgs a;
         a.y = yd; a.h = hb; a.doff = d_doff; a.active = d_active; a.n_files = F; a.window = P->env_window;
-        a.env = O->env;
+        a.env = O->env; a.skip = d_fused;
         LAUNCH(ctx, s, "k_native_env", k_native_env, dim3((unsigned)((maxnd + NE_T - 1) / NE_T), F), dim3(NE_T), 0,
                s, a);
     }

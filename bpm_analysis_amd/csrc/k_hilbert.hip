@@ -1,0 +1,285 @@
+/*
+ * k_hilbert.hip — native-mode envelope after the filter, fused in LDS:
+ *   env = centred rolling mean (window sr//10) of |scipy.signal.hilbert(yd)|
+ * oracle: scipy/signal/_signaltools.py:2318 (hilbert: ifft(fft(x) * h),
+ * h = 1, 2, ..., 2, 1, 0, ...), oracle/oracle.py hilbert_abs + rolling_mean.
+ *
+ * One workgroup per recording; the recording's whole transform stays in LDS.
+ * The real signal y (Nd = N = 2M samples) is read as M complex points
+ * z_m = y_2m + i y_2m+1 (its natural memory layout), then
+ *   1. forward mixed-radix DIF over M: natural order in, digit-reversed out,
+ *      in place (no permutation pass);
+ *   2. one pointwise pass over the pairs (k, M - k) turns Z = DFT_M(z) into
+ *      X_k = conj(w) S - w D  (w = e^(-2 pi i k / N), S = Z_k + conj(Z_(M-k)),
+ *      D = Z_k - conj(Z_(M-k)), X_0 = 0): the half-length spectrum whose
+ *      inverse DFT is c_2m + i c_2m+1, with c = N * Im(analytic signal) — the
+ *      "-i on the positive half spectrum, zero DC and Nyquist" of hilbert,
+ *      folded together with the real-FFT split and merge;
+ *   3. inverse mixed-radix DIT: digit-reversed in, natural order out;
+ *   4. |analytic| = sqrt(y^2 + (c/N)^2) in place, then the rolling mean.
+ * Radix 2 butterflies are plain; odd primes p use the pair-symmetric direct
+ * DFT X_k = x_0 + sum_n (x_n + x_(p-n)) cos(2 pi n k/p) -/+ i (x_n - x_(p-n))
+ * sin(2 pi n k/p) (a quarter of the multiplies of the plain DFT), with the
+ * cos/sin advanced by rotation and re-seeded from the exact table every 16
+ * steps.  Twiddles W_N^e = hi[e >> 7] * lo[e & 127] (tables in LDS).
+ * Recordings whose M does not factor into primes <= HB_PMAX or does not fit
+ * in LDS take the rocFFT path (k_envelope_native.hip).
+ */
+#include "bpmx_common.h"
+#include "bpmx_hilbert.h"
+
+namespace bpmx {
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(__builtin_fma(a.x, b.x, -a.y * b.y), __builtin_fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {          /* a * conj(b) */
+    return make_double2(__builtin_fma(a.x, b.x, a.y * b.y), __builtin_fma(a.y, b.x, -a.x * b.y));
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+struct HbLds {
+    double2 *x, *twh, *twl, *pt;
+    __device__ __forceinline__ double2 tw(int e) const { return cmul(twh[e >> 7], twl[e & 127]); }   /* W_N^e */
+};
+
+/* radix-2 stage: DIF (twiddle after) or DIT inverse (conjugate twiddle before) */
+template <bool INV>
+__device__ __forceinline__ void hb_radix2(const HbLds &S, int M, int N, int B, int L) {
+    const int nb = M / 2, step = N / B;
+    for (int t = threadIdx.x; t < nb; t += HB_T) {
+        const int blk = t / L, n2 = t - blk * L, base = blk * B + n2;
+        double2 a = S.x[base], b = S.x[base + L];
+        if (!INV) {
+            const double2 d = csub(a, b);
+            S.x[base] = cadd(a, b);
+            S.x[base + L] = n2 ? cmul(d, S.tw(step * n2)) : d;
+        } else {
+            if (n2) b = cmulc(b, S.tw(step * n2));
+            S.x[base] = cadd(a, b);
+            S.x[base + L] = csub(a, b);
+        }
+    }
+    __syncthreads();
+}
+
+/* odd prime radix p, pair-symmetric direct DFT */
+template <bool INV>
+__device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, int L, int p, const double2 *ct) {
+    const int h = (p - 1) >> 1, nbf = M / p, step = N / B;
+    /* pre-pass: (DIT: conjugate twiddles, then) x_n, x_(p-n) -> a_n = x_n + x_(p-n), b_n = x_n - x_(p-n) */
+    for (int t = threadIdx.x; t < nbf * h; t += HB_T) {
+        const int bf = t / h, n = t - bf * h + 1;
+        const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+        double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
+        if (INV && n2) {
+            u = cmulc(u, S.tw(step * n2 * n));
+            v = cmulc(v, S.tw(step * n2 * (p - n)));
+        }
+        S.x[base + n * L] = cadd(u, v);
+        S.x[base + (p - n) * L] = csub(u, v);
+    }
+    __syncthreads();
+    /* outputs k and p - k of every butterfly, kept in registers until all reads are done */
+    const int ntask = nbf * (h + 1);
+    double2 r0[HB_MAXT], r1[HB_MAXT];
+#pragma unroll
+    for (int i = 0; i < HB_MAXT; ++i) {
+        const int t = threadIdx.x + i * HB_T;
+        if (t < ntask) {
+            const int bf = t / (h + 1), k = t - bf * (h + 1);
+            const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+            const double2 x0 = S.x[base];
+            double2 A = make_double2(0.0, 0.0), Bs = make_double2(0.0, 0.0);
+            if (k == 0) {
+                for (int n = 1; n <= h; ++n) A = cadd(A, S.x[base + n * L]);
+            } else {
+                const double2 rot = ct[k];                    /* (cos, sin)(2 pi k / p) */
+                double c = 0, s = 0;
+                int idx = 0;
+                for (int n = 1; n <= h; ++n) {
+                    idx += k;
+                    if (idx >= p) idx -= p;
+                    if (((n - 1) & 15) == 0) {                /* exact re-seed every 16 steps */
+                        const double2 e = ct[idx];
+                        c = e.x; s = e.y;
+                    } else {
+                        const double cn = __builtin_fma(c, rot.x, -s * rot.y);
+                        s = __builtin_fma(s, rot.x, c * rot.y);
+                        c = cn;
+                    }
+                    const double2 a = S.x[base + n * L], b = S.x[base + (p - n) * L];
+                    A.x = __builtin_fma(a.x, c, A.x); A.y = __builtin_fma(a.y, c, A.y);
+                    Bs.x = __builtin_fma(b.x, s, Bs.x); Bs.y = __builtin_fma(b.y, s, Bs.y);
+                }
+            }
+            /* forward: X_k = x0 + A - iB, X_(p-k) = x0 + A + iB; inverse: signs swapped */
+            const double2 xa = cadd(x0, A);
+            const double2 mib = INV ? make_double2(-Bs.y, Bs.x) : make_double2(Bs.y, -Bs.x);   /* -+ iB */
+            r0[i] = cadd(xa, mib);
+            r1[i] = csub(xa, mib);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < HB_MAXT; ++i) {
+        const int t = threadIdx.x + i * HB_T;
+        if (t < ntask) {
+            const int bf = t / (h + 1), k = t - bf * (h + 1);
+            const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+            if (!INV && n2) {
+                S.x[base + k * L] = k ? cmul(r0[i], S.tw(step * n2 * k)) : r0[i];
+                if (k) S.x[base + (p - k) * L] = cmul(r1[i], S.tw(step * n2 * (p - k)));
+            } else {
+                S.x[base + k * L] = r0[i];
+                if (k) S.x[base + (p - k) * L] = r1[i];
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int hb_pos(const HilbPlan &P, int k) {     /* position of frequency k after the DIF */
+    int pos = 0;
+    for (int i = 0; i < P.ns; ++i) {
+        const int r = P.rad[i], q = k / r;
+        pos += (k - q * r) * P.L[i];
+        k = q;
+    }
+    return pos;
+}
+
+__global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
+    const int f = A.f_begin + blockIdx.x;
+    if (f >= A.f_end || !A.active[f]) return;
+    extern __shared__ __align__(16) double2 hb_smem[];
+    const int M = P.M, N = P.N;
+    HbLds S;
+    S.x = hb_smem;
+    S.twh = S.x + M;
+    S.twl = S.twh + P.ntwh;
+    S.pt = S.twl + 128;
+    const int64_t d0 = A.doff[f];
+    const double2 *y2 = (const double2 *)(A.yd + d0);              /* doff is even: 16-B aligned (host checks) */
+    for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab; i += HB_T) S.twh[i] = A.tabs[i];
+    for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2[m];
+    __syncthreads();
+
+    for (int i = 0; i < P.ns; ++i) {
+        if (P.rad[i] == 2) hb_radix2<false>(S, M, N, P.B[i], P.L[i]);
+        else hb_radixp<false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
+    }
+    /* pointwise: pairs (k, M - k), k = 0 .. M/2 */
+    for (int k = threadIdx.x; k <= M / 2; k += HB_T) {
+        if (k == 0) {
+            S.x[0] = make_double2(0.0, 0.0);                        /* pos(0) = 0: DC and Nyquist of the Hilbert spectrum */
+            continue;
+        }
+        const int km = M - k;
+        const int pk = hb_pos(P, k), pm = hb_pos(P, km);
+        const double2 zk = S.x[pk], zm = S.x[pm];
+        auto xk = [&](double2 za, double2 zb, int kk) {              /* X_kk from Z_kk, Z_(M-kk) */
+            const double2 cb = make_double2(zb.x, -zb.y);
+            const double2 Sm = cadd(za, cb), D = csub(za, cb), w = S.tw(kk);
+            return csub(cmulc(Sm, w), cmul(w, D));
+        };
+        const double2 xa = xk(zk, zm, k);
+        if (km != k) S.x[pm] = xk(zm, zk, km);
+        S.x[pk] = xa;
+    }
+    __syncthreads();
+    for (int i = P.ns - 1; i >= 0; --i) {
+        if (P.rad[i] == 2) hb_radix2<true>(S, M, N, P.B[i], P.L[i]);
+        else hb_radixp<true>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
+    }
+    /* |analytic| = sqrt(y^2 + (c/N)^2), in place (two reals per complex slot) */
+    const double inv = 1.0 / (double)N;
+    for (int m = threadIdx.x; m < M; m += HB_T) {
+        const double2 c = S.x[m], y = y2[m];
+        const double i0 = c.x * inv, i1 = c.y * inv;
+        S.x[m] = make_double2(sqrt(y.x * y.x + i0 * i0), sqrt(y.y * y.y + i1 * i1));
+    }
+    __syncthreads();
+    const double *mag = (const double *)S.x;
+    const int64_t w = P.window;
+    double *env = A.env + d0;
+    for (int i = threadIdx.x; i < N; i += HB_T) {
+        int64_t s, e;
+        win_bounds(i, N, w, s, e);
+        double sum = 0.0;
+        for (int64_t q = s; q < e; ++q) sum += mag[q];
+        env[i] = sum / (double)(e - s);
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* host: plan + tables (long double), cached per N */
+int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes) {
+    if (nd < 4 || (nd & 1)) return 0;
+    const int64_t M = nd / 2;
+    int rad[HB_MAXS], ns = 0;
+    int64_t m = M;
+    while (m % 2 == 0) {
+        if (ns == HB_MAXS) return 0;
+        rad[ns++] = 2;
+        m /= 2;
+    }
+    for (int64_t p = 3; m > 1; p += 2) {
+        if (p > HB_PMAX) return 0;
+        while (m % p == 0) {
+            if (ns == HB_MAXS) return 0;
+            rad[ns++] = (int)p;
+            m /= p;
+        }
+    }
+    std::memset(P, 0, sizeof(*P));
+    P->M = (int32_t)M;
+    P->N = (int32_t)nd;
+    P->ns = ns;
+    P->ntwh = (int32_t)((nd + 127) / 128);
+    P->window = window;
+    int64_t B = M;
+    std::vector<int> primes;
+    for (int i = 0; i < ns; ++i) {
+        const int r = rad[i];
+        P->rad[i] = r;
+        P->B[i] = (int32_t)B;
+        P->L[i] = (int32_t)(B / r);
+        B /= r;
+        if (r > 2) {
+            /* register-held outputs: (M / p) (h + 1) tasks over HB_T threads */
+            if ((M / r) * ((r + 1) / 2) > (int64_t)HB_T * HB_MAXT) return 0;
+            int off = -1, acc = 0;
+            for (int q : primes) { if (q == r) off = acc; acc += q; }
+            if (off < 0) { off = acc; primes.push_back(r); }
+            P->ptab[i] = off;
+        } else {
+            P->ptab[i] = -1;
+        }
+    }
+    int np = 0;
+    for (int q : primes) np += q;
+    P->nptab = np;
+    *lds_bytes = (size_t)(M + P->ntwh + 128 + np) * sizeof(double2);
+    if (*lds_bytes > HB_LDS_MAX) return 0;
+    tabs->resize((size_t)P->ntwh + 128 + np);
+    const long double tp = 6.283185307179586476925286766559005768L;
+    for (int j = 0; j < P->ntwh; ++j) {
+        const long double a = -tp * (long double)(128LL * j) / (long double)nd;
+        (*tabs)[j] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    for (int j = 0; j < 128; ++j) {
+        const long double a = -tp * (long double)j / (long double)nd;
+        (*tabs)[P->ntwh + j] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    int o = P->ntwh + 128;
+    for (int q : primes)
+        for (int j = 0; j < q; ++j, ++o) {
+            const long double a = tp * (long double)j / (long double)q;
+            (*tabs)[o] = make_double2((double)cosl(a), (double)sinl(a));
+        }
+    return 1;
+}
+
+}  // namespace bpmx

@@ -72,8 +72,10 @@ enum bpmx_file_flag {
 enum bpmx_option {
     BPMX_OPT_ROLLQ_MERGE = 1, /* force the sorted-union rolling quantile (test/diagnostic; default picks the
                                  wavelet-matrix kernel for recordings of <= 20480 decimated samples) */
-    BPMX_OPT_NATIVE_F64 = 2   /* native mode: f64 VALU block projections instead of the exact-integer
+    BPMX_OPT_NATIVE_F64 = 2,  /* native mode: f64 VALU block projections instead of the exact-integer
                                  matrix-core kernel (test/diagnostic) */
+    BPMX_OPT_HILBERT_ROCFFT = 4 /* native mode: rocFFT R2C/C2R Hilbert instead of the fused in-LDS transform
+                                   (test/diagnostic; recordings the fused kernel cannot plan always use it) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

@@ -230,3 +230,30 @@ def test_native_block_kernels_agree(det, fs):
         assert ea <= 1e-9 * scale
         _check_file(a, o, exact_env=False)
         _check_file(b, o, exact_env=False)
+
+
+def test_fused_hilbert_matches_rocfft_and_oracle(det):
+    """k_hilbert_env (in-LDS mixed-radix transform + rolling mean) against the
+    rocFFT path (BPMX_OPT_HILBERT_ROCFFT) and the oracle, on a ragged batch whose
+    Nd exercise radix 2 / 3 / 5 / 23 / 197 / 401 plans, a tiny plan, and odd or
+    large-prime Nd that fall back to rocFFT inside the same batch."""
+    import torch
+    from bpm_analysis_amd import _native as N
+    fs, ds = 44100, 146
+    nds = [18124, 9000, 2406, 1000, 18, 402, 12083, 6038]
+    lens = [nd * ds - (i % 3) for i, nd in enumerate(nds)]
+    recs = [O.synth(700 + i, n, fs, 1) for i, n in enumerate(lens)]
+    dev = torch.from_numpy(np.concatenate(recs)).to(det.device)
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    outs = []
+    for opt in (0, N.OPT_HILBERT_ROCFFT):
+        res = det.run(dev, fo, fs, params, mode="native", want_y=True, options=opt)
+        torch.cuda.synchronize()
+        outs.append(res.to_host())
+    for a, b, pcm in zip(outs[0], outs[1], recs):
+        scale = np.max(np.abs(b["env"]))
+        assert np.max(np.abs(a["env"] - b["env"])) <= 1e-12 * scale
+        if len(pcm) > 5000 * ds:
+            o = O.detect(pcm, fs, params, mode="native")
+            _check_file(a, o, exact_env=False)

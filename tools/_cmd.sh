@@ -1,5 +1,5 @@
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "native" > gpurun_out/pt_native.log 2>&1 || { tail -30 gpurun_out/pt_native.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "native or hilbert" > gpurun_out/pt_native.log 2>&1 || { tail -40 gpurun_out/pt_native.log; exit 1; }
 tail -2 gpurun_out/pt_native.log
 for o in 0; do
 timeout -k 10 300 python bench.py --no-cpu --pcie-steps 0 --options $o > gpurun_out/bench_o$o.log 2>&1 || exit 1
