@@ -13,7 +13,9 @@
 namespace bpmx {
 
 constexpr int HB_T = 1024;                 /* threads per recording */
-constexpr int HB_MAXT = 6;                 /* register-held butterfly outputs per thread per stage */
+constexpr int HB_KB = 3;                   /* frequencies per butterfly task (odd prime radices) */
+constexpr int HB_MAXT = 2;                 /* tasks (HB_KB register-held output pairs each) per thread per stage */
+constexpr int HB_RMPER = 20;               /* rolling-mean outputs per thread: Nd <= HB_T * HB_RMPER */
 constexpr int HB_MAXS = 16;                /* radix stages */
 constexpr int HB_PMAX = 401;               /* largest prime radix (direct DFT cost ~ M p / 2 FMA per stage) */
 constexpr size_t HB_LDS_MAX = 160 * 1024;  /* one workgroup per CU */
@@ -30,6 +32,7 @@ struct HilbArgs {
     int32_t f_begin, f_end;        /* a run of recordings with this plan's Nd */
     const double2 *tabs;           /* twiddle hi [ntwh] | lo [128] | prime cos/sin tables */
     double *env;
+    unsigned long long *stamps;    /* tools/hbench phase timing only (nullptr) */
 };
 
 __global__ void k_hilbert_env(HilbArgs A, HilbPlan P);

@@ -1201,7 +1201,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             if (even) {
                 HilbArgs a;
                 a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
-                a.tabs = ht->dev; a.env = O->env;
+                a.tabs = ht->dev; a.env = O->env; a.stamps = nullptr;
                 (void)hipFuncSetAttribute((const void *)k_hilbert_env, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)hlds);
                 LAUNCH(ctx, s, "k_hilbert_env", k_hilbert_env, dim3((unsigned)(f1 - f0)), dim3(HB_T), hlds, s, a, hp);

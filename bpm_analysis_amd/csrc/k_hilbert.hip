@@ -27,6 +27,7 @@
  */
 #include "bpmx_common.h"
 #include "bpmx_hilbert.h"
+#include "bpmx_stamps.h"
 
 namespace bpmx {
 
@@ -81,44 +82,81 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
         S.x[base + (p - n) * L] = csub(u, v);
     }
     __syncthreads();
-    /* outputs k and p - k of every butterfly, kept in registers until all reads are done */
-    const int ntask = nbf * (h + 1);
-    double2 r0[HB_MAXT], r1[HB_MAXT];
+    /* Outputs k and p - k of every butterfly, HB_KB consecutive k per task so
+     * one pair of LDS reads (a_n, b_n) feeds HB_KB frequencies; kept in
+     * registers until every task of the stage has read its inputs.  cos and
+     * sin of n k (2 pi / p) advance by the two-term recurrence
+     * c_(n+1) = 2 cos(k 2pi/p) c_n - c_(n-1) (one FMA each), re-seeded from
+     * the exact table every 16 steps. */
+    const int ng = (h + HB_KB) / HB_KB;                       /* k groups: k = 0 .. h */
+    const int ntask = nbf * ng;
+    double2 r0[HB_MAXT][HB_KB], r1[HB_MAXT][HB_KB];
 #pragma unroll
     for (int i = 0; i < HB_MAXT; ++i) {
         const int t = threadIdx.x + i * HB_T;
         if (t < ntask) {
-            const int bf = t / (h + 1), k = t - bf * (h + 1);
+            const int bf = t / ng, k0 = (t - bf * ng) * HB_KB;
             const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
             const double2 x0 = S.x[base];
-            double2 A = make_double2(0.0, 0.0), Bs = make_double2(0.0, 0.0);
-            if (k == 0) {
-                for (int n = 1; n <= h; ++n) A = cadd(A, S.x[base + n * L]);
-            } else {
-                const double2 rot = ct[k];                    /* (cos, sin)(2 pi k / p) */
-                double c = 0, s = 0;
-                int idx = 0;
-                for (int n = 1; n <= h; ++n) {
-                    idx += k;
-                    if (idx >= p) idx -= p;
-                    if (((n - 1) & 15) == 0) {                /* exact re-seed every 16 steps */
-                        const double2 e = ct[idx];
-                        c = e.x; s = e.y;
-                    } else {
-                        const double cn = __builtin_fma(c, rot.x, -s * rot.y);
-                        s = __builtin_fma(s, rot.x, c * rot.y);
-                        c = cn;
+            double ax[HB_KB], ay[HB_KB], bx[HB_KB], by[HB_KB], c[HB_KB], cp[HB_KB], sn[HB_KB], sp[HB_KB], c2[HB_KB];
+            int idx[HB_KB];
+#pragma unroll
+            for (int j = 0; j < HB_KB; ++j) {
+                ax[j] = ay[j] = bx[j] = by[j] = 0.0;
+                c[j] = sn[j] = cp[j] = sp[j] = 0.0;
+                idx[j] = 0;
+                const int k = k0 + j <= h ? k0 + j : 0;
+                c2[j] = 2.0 * ct[k].x;
+            }
+            for (int n0 = 1; n0 <= h; n0 += 16) {
+                /* seed: (c, s) at n0 - 1 and n0 for every k of the group */
+#pragma unroll
+                for (int j = 0; j < HB_KB; ++j) {
+                    const int k = k0 + j <= h ? k0 + j : 0;
+                    int i1 = idx[j] + k;                           /* (n0 k) mod p; idx = ((n0 - 1) k) mod p */
+                    if (i1 >= p) i1 -= p;
+                    const double2 e0 = ct[idx[j]], e1 = ct[i1];
+                    cp[j] = e0.x; sp[j] = e0.y; c[j] = e1.x; sn[j] = e1.y;
+                    int i16 = i1 + 15 * k;                         /* ((n0 + 15) k) mod p */
+                    i16 -= (i16 / p) * p;
+                    idx[j] = i16;
+                }
+                const int n1 = n0 + 16 <= h + 1 ? n0 + 16 : h + 1;
+                /* two steps per trip: the recurrence alternates between (c, cp)
+                 * and (cp, c), so no register rotation moves */
+                int n = n0;
+                for (; n + 1 < n1; n += 2) {
+                    const double2 a0 = S.x[base + n * L], b0 = S.x[base + (p - n) * L];
+                    const double2 a1 = S.x[base + (n + 1) * L], b1 = S.x[base + (p - n - 1) * L];
+#pragma unroll
+                    for (int j = 0; j < HB_KB; ++j) {
+                        ax[j] = __builtin_fma(a0.x, c[j], ax[j]); ay[j] = __builtin_fma(a0.y, c[j], ay[j]);
+                        bx[j] = __builtin_fma(b0.x, sn[j], bx[j]); by[j] = __builtin_fma(b0.y, sn[j], by[j]);
+                        cp[j] = __builtin_fma(c2[j], c[j], -cp[j]);       /* cos (n+1) k */
+                        sp[j] = __builtin_fma(c2[j], sn[j], -sp[j]);
+                        ax[j] = __builtin_fma(a1.x, cp[j], ax[j]); ay[j] = __builtin_fma(a1.y, cp[j], ay[j]);
+                        bx[j] = __builtin_fma(b1.x, sp[j], bx[j]); by[j] = __builtin_fma(b1.y, sp[j], by[j]);
+                        c[j] = __builtin_fma(c2[j], cp[j], -c[j]);        /* cos (n+2) k */
+                        sn[j] = __builtin_fma(c2[j], sp[j], -sn[j]);
                     }
-                    const double2 a = S.x[base + n * L], b = S.x[base + (p - n) * L];
-                    A.x = __builtin_fma(a.x, c, A.x); A.y = __builtin_fma(a.y, c, A.y);
-                    Bs.x = __builtin_fma(b.x, s, Bs.x); Bs.y = __builtin_fma(b.y, s, Bs.y);
+                }
+                if (n < n1) {
+                    const double2 a0 = S.x[base + n * L], b0 = S.x[base + (p - n) * L];
+#pragma unroll
+                    for (int j = 0; j < HB_KB; ++j) {
+                        ax[j] = __builtin_fma(a0.x, c[j], ax[j]); ay[j] = __builtin_fma(a0.y, c[j], ay[j]);
+                        bx[j] = __builtin_fma(b0.x, sn[j], bx[j]); by[j] = __builtin_fma(b0.y, sn[j], by[j]);
+                    }
                 }
             }
             /* forward: X_k = x0 + A - iB, X_(p-k) = x0 + A + iB; inverse: signs swapped */
-            const double2 xa = cadd(x0, A);
-            const double2 mib = INV ? make_double2(-Bs.y, Bs.x) : make_double2(Bs.y, -Bs.x);   /* -+ iB */
-            r0[i] = cadd(xa, mib);
-            r1[i] = csub(xa, mib);
+#pragma unroll
+            for (int j = 0; j < HB_KB; ++j) {
+                const double2 xa = make_double2(x0.x + ax[j], x0.y + ay[j]);
+                const double2 mib = INV ? make_double2(-by[j], bx[j]) : make_double2(by[j], -bx[j]);   /* -+ iB */
+                r0[i][j] = cadd(xa, mib);
+                r1[i][j] = csub(xa, mib);
+            }
         }
     }
     __syncthreads();
@@ -126,14 +164,19 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
     for (int i = 0; i < HB_MAXT; ++i) {
         const int t = threadIdx.x + i * HB_T;
         if (t < ntask) {
-            const int bf = t / (h + 1), k = t - bf * (h + 1);
+            const int bf = t / ng, k0 = (t - bf * ng) * HB_KB;
             const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
-            if (!INV && n2) {
-                S.x[base + k * L] = k ? cmul(r0[i], S.tw(step * n2 * k)) : r0[i];
-                if (k) S.x[base + (p - k) * L] = cmul(r1[i], S.tw(step * n2 * (p - k)));
-            } else {
-                S.x[base + k * L] = r0[i];
-                if (k) S.x[base + (p - k) * L] = r1[i];
+#pragma unroll
+            for (int j = 0; j < HB_KB; ++j) {
+                const int k = k0 + j;
+                if (k > h) break;
+                if (!INV && n2) {
+                    S.x[base + k * L] = k ? cmul(r0[i][j], S.tw(step * n2 * k)) : r0[i][j];
+                    if (k) S.x[base + (p - k) * L] = cmul(r1[i][j], S.tw(step * n2 * (p - k)));
+                } else {
+                    S.x[base + k * L] = r0[i][j];
+                    if (k) S.x[base + (p - k) * L] = r1[i][j];
+                }
             }
         }
     }
@@ -165,10 +208,12 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab; i += HB_T) S.twh[i] = A.tabs[i];
     for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2[m];
     __syncthreads();
-
+    STAMP_DECL
+    STAMP(0);
     for (int i = 0; i < P.ns; ++i) {
         if (P.rad[i] == 2) hb_radix2<false>(S, M, N, P.B[i], P.L[i]);
         else hb_radixp<false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
+        STAMP(i < 3 ? 1 + i : 3);
     }
     /* pointwise: pairs (k, M - k), k = 0 .. M/2 */
     for (int k = threadIdx.x; k <= M / 2; k += HB_T) {
@@ -189,10 +234,12 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         S.x[pk] = xa;
     }
     __syncthreads();
+    STAMP(4);
     for (int i = P.ns - 1; i >= 0; --i) {
         if (P.rad[i] == 2) hb_radix2<true>(S, M, N, P.B[i], P.L[i]);
         else hb_radixp<true>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
     }
+    STAMP(5);
     /* |analytic| = sqrt(y^2 + (c/N)^2), in place (two reals per complex slot) */
     const double inv = 1.0 / (double)N;
     for (int m = threadIdx.x; m < M; m += HB_T) {
@@ -201,16 +248,45 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         S.x[m] = make_double2(sqrt(y.x * y.x + i0 * i0), sqrt(y.y * y.y + i1 * i1));
     }
     __syncthreads();
+    STAMP(6);
+    /* centred rolling mean (min_periods 1): each thread a contiguous run of
+     * outputs, the window sum slid along it (one direct sum per run) */
     const double *mag = (const double *)S.x;
     const int64_t w = P.window;
     double *env = A.env + d0;
-    for (int i = threadIdx.x; i < N; i += HB_T) {
+    const int per = (N + HB_T - 1) / HB_T;                 /* <= HB_RMPER (host checks) */
+    const int i0 = threadIdx.x * per, i1 = i0 + per < N ? i0 + per : N;
+    double ev[HB_RMPER];
+    if (i0 < i1) {
         int64_t s, e;
-        win_bounds(i, N, w, s, e);
+        win_bounds(i0, N, w, s, e);
         double sum = 0.0;
         for (int64_t q = s; q < e; ++q) sum += mag[q];
-        env[i] = sum / (double)(e - s);
+        ev[0] = sum / (double)(e - s);
+#pragma unroll
+        for (int j = 1; j < HB_RMPER; ++j) {
+            const int i = i0 + j;
+            if (i < i1) {
+                int64_t s2, e2;
+                win_bounds(i, N, w, s2, e2);
+                for (int64_t q = e; q < e2; ++q) sum += mag[q];
+                for (int64_t q = s; q < s2; ++q) sum -= mag[q];
+                s = s2; e = e2;
+                ev[j] = sum / (double)(e - s);
+            }
+        }
     }
+    /* through LDS, so the global stores are coalesced */
+    __syncthreads();
+    double *stage = (double *)S.x;
+#pragma unroll
+    for (int j = 0; j < HB_RMPER; ++j)
+        if (i0 + j < i1) stage[i0 + j] = ev[j];
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += HB_T) env[i] = stage[i];
+    __syncthreads();
+    STAMP(7);
+    STAMP_FLUSH(A.stamps);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -248,8 +324,8 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
         P->L[i] = (int32_t)(B / r);
         B /= r;
         if (r > 2) {
-            /* register-held outputs: (M / p) (h + 1) tasks over HB_T threads */
-            if ((M / r) * ((r + 1) / 2) > (int64_t)HB_T * HB_MAXT) return 0;
+            /* register-held outputs: (M / p) ceil((h + 1) / HB_KB) tasks over HB_T threads */
+            if ((M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT) return 0;
             int off = -1, acc = 0;
             for (int q : primes) { if (q == r) off = acc; acc += q; }
             if (off < 0) { off = acc; primes.push_back(r); }
@@ -261,6 +337,7 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
     int np = 0;
     for (int q : primes) np += q;
     P->nptab = np;
+    if ((nd + HB_T - 1) / HB_T > HB_RMPER) return 0;
     *lds_bytes = (size_t)(M + P->ntwh + 128 + np) * sizeof(double2);
     if (*lds_bytes > HB_LDS_MAX) return 0;
     tabs->resize((size_t)P->ntwh + 128 + np);

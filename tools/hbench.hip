@@ -1,0 +1,63 @@
+/*
+ * hbench.hip — standalone phase timing of k_hilbert_env (s_memtime stamps,
+ * thread 0 of each workgroup): load | fwd stage 0 | 1 | 2 | pointwise | inverse | |z| | rolling mean.
+ *   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/hbench.hip -o tools/hbench
+ *   ./tools/hbench [files] [nd]
+ */
+#define BPMX_STAMPS 1
+#include "../bpm_analysis_amd/csrc/k_hilbert.hip"
+
+#include <cstdio>
+#include <cstdlib>
+
+using namespace bpmx;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+int main(int argc, char **argv) {
+    const int F = argc > 1 ? atoi(argv[1]) : 1024;
+    const int64_t nd = argc > 2 ? atoll(argv[2]) : 18124;
+    HilbPlan P;
+    std::vector<double2> tabs;
+    size_t lds = 0;
+    if (!hilbert_plan(nd, 30, &P, &tabs, &lds)) { printf("no plan\n"); return 1; }
+    printf("nd %lld M %d stages", (long long)nd, P.M);
+    for (int i = 0; i < P.ns; ++i) printf(" %d", P.rad[i]);
+    printf(" lds %zu\n", lds);
+    std::vector<double> y((size_t)F * nd);
+    unsigned long long s = 1;
+    for (auto &v : y) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (double)(s >> 11) / 9007199254740992.0 - 0.5; }
+    std::vector<int64_t> doff(F + 1);
+    for (int f = 0; f <= F; ++f) doff[f] = (int64_t)f * nd;
+    std::vector<int32_t> act(F, 1);
+    double *dy, *denv; int64_t *dd; int32_t *da; double2 *dt; unsigned long long *dst;
+    CK(hipMalloc(&dy, y.size() * 8)); CK(hipMalloc(&denv, y.size() * 8)); CK(hipMalloc(&dd, (F + 1) * 8));
+    CK(hipMalloc(&da, F * 4)); CK(hipMalloc(&dt, tabs.size() * 16)); CK(hipMalloc(&dst, (size_t)F * 64));
+    CK(hipMemcpy(dy, y.data(), y.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dd, doff.data(), (F + 1) * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(da, act.data(), F * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt, tabs.data(), tabs.size() * 16, hipMemcpyHostToDevice));
+    HilbArgs a{dy, dd, da, 0, F, dt, denv, dst};
+    CK(hipFuncSetAttribute((const void *)k_hilbert_env, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int it = 0; it < 3; ++it) hipLaunchKernelGGL(k_hilbert_env, dim3(F), dim3(HB_T), lds, 0, a, P);
+    CK(hipDeviceSynchronize());
+    const int R = 10;
+    CK(hipEventRecord(e0));
+    for (int it = 0; it < R; ++it) hipLaunchKernelGGL(k_hilbert_env, dim3(F), dim3(HB_T), lds, 0, a, P);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> st((size_t)F * 8);
+    CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
+    double acc[8] = {0};
+    for (int f = 0; f < F; ++f) for (int k = 0; k < 8; ++k) acc[k] += (double)st[(size_t)f * 8 + k];
+    printf("kernel %.4f ms;  mean cycles per workgroup (s_memtime):", ms / R);
+    const char *nm[8] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "rollmean"};
+    double tot = 0;
+    for (int k = 0; k < 8; ++k) tot += acc[k] / F;
+    for (int k = 0; k < 8; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
+    printf("\n");
+    return 0;
+}
