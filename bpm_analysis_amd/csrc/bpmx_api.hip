@@ -379,14 +379,36 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1;
             LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
         }
-        if ((rc = rollq(d_run1, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
+        /* Draft floor: sanitize reads it at the raw troughs only, so the
+         * recordings whose every keep decision follows from k_draft_bounds'
+         * bracket skip the full rolling quantile; the others (and, after
+         * sanitize, bounded ones left with <= 2 troughs, whose floor IS the
+         * draft) get it exactly.  BPMX_OPT_DRAFT_FULL forces it for all. */
+        const bool bounds = !(P->options & BPMX_OPT_DRAFT_FULL);
+        uint8_t *tdec = nullptr;
+        int32_t *d_exact = d_run1, *d_runfb = nullptr;
+        if (bounds) {
+            tdec = (uint8_t *)ctx->buf("trough_dec", (size_t)sumnd, &rc);
+            int32_t *fl2 = (int32_t *)ctx->buf("draft_masks", (size_t)F * 8, &rc);
+            if (rc != BPMX_OK) return rc;
+            d_exact = fl2;
+            d_runfb = fl2 + F;
+            HIP_TRY(hipMemsetAsync(d_exact, 0, (size_t)F * 4, s));
+            DraftBoundArgs a;
+            a.env = O->env; a.doff = d_doff; a.raw = rawt; a.nraw = d_nraw; a.run = d_run1; a.n_files = F;
+            a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
+            a.dec = tdec; a.exact = d_exact;
+            LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F), dim3(DB_T), 0, s, a);
+        }
+        if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {
             SanitizeArgs a;
             a.env = O->env; a.draft = draft; a.doff = d_doff; a.active = d_active; a.raw = rawt; a.nraw = d_nraw;
             a.n_files = F; a.mult = P->reject_mult; a.out = O->troughs; a.nout = O->n_troughs; a.flags = O->flags;
-            a.run2 = d_run2;
+            a.run2 = d_run2; a.dec = tdec; a.exact = d_exact; a.run_fb = d_runfb;
             LAUNCH(ctx, s, "k_sanitize", k_sanitize, dim3(F), dim3(256), 0, s, a);
         }
+        if (bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {
             InterpArgs a;
             a.env = O->env; a.doff = d_doff; a.troughs = O->troughs; a.ntr = O->n_troughs; a.run = d_run2;

@@ -112,7 +112,29 @@ struct SanitizeArgs {
     int32_t *nout;
     int32_t *flags;
     int32_t *run2;           /* [F] files that need the second floor pass */
+    const uint8_t *dec;      /* [raw trough j at doff + j] keep decision of k_draft_bounds (nullptr: use draft) */
+    const int32_t *exact;    /* [F] 1: draft computed in full, decide from it instead */
+    int32_t *run_fb;         /* [F] out: draft floor kept (<= 2 troughs) but only bounded: compute it in full */
 };
+
+/* k_draft_bounds: the draft floor (first rolling quantile) is read only at the
+ * raw troughs (sanitize) unless <= 2 troughs survive.  Its dense input is
+ * piecewise linear between the troughs, so every window's k-th smallest value
+ * is bracketed by weighted order statistics of the segments' end values;
+ * most troughs' keep decision follows from the bracket alone. */
+struct DraftBoundArgs {
+    const double *env;
+    const int64_t *doff;
+    const int64_t *raw;      /* raw troughs */
+    const int32_t *nraw;
+    const int32_t *run;      /* [F] files with >= 5 raw troughs */
+    int32_t n_files, window, min_periods;
+    double q, mult;
+    uint8_t *dec;            /* [doff + j]: 1 keep, 0 reject, 2 undecided */
+    int32_t *exact;          /* [F] out: 1 = needs the full draft (undecided trough, all-NaN draft, too many troughs) */
+};
+constexpr int DB_T = 256;
+constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */
 
 struct FinalArgs {
     const double *draft;
@@ -143,6 +165,7 @@ __global__ void k_block_stats(BlockStatArgs A);
 __global__ void k_find_peaks(PeakArgs A);
 __global__ void k_interp(InterpArgs A);
 __global__ void k_sanitize(SanitizeArgs A);
+__global__ void k_draft_bounds(DraftBoundArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);

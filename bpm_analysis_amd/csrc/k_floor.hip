@@ -357,6 +357,7 @@ __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
         return;
     }
     const double *env = A.env + d0, *draft = A.draft + d0;
+    const bool exact = !A.dec || A.exact[f];
     int w = 0;
     for (int c0 = 0; c0 < m; c0 += 256) {
         const int j = c0 + tid;
@@ -364,8 +365,12 @@ __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
         int64_t t = 0;
         if (j < m) {
             t = raw[j];
-            const double fl = draft[t];
-            keep = (fl == fl) && env[t] <= A.mult * fl;
+            if (exact) {
+                const double fl = draft[t];
+                keep = (fl == fl) && env[t] <= A.mult * fl;
+            } else {
+                keep = A.dec[d0 + j] == 1;
+            }
         }
         int tot;
         const int off = block_scan_flag<256>(keep, sh, &tot);
@@ -376,7 +381,126 @@ __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
         A.nout[f] = w;
         if (w <= 2) A.flags[f] |= BPMX_F_DRAFT_FLOOR;
         A.run2[f] = w > 2 ? 1 : 0;
+        if (A.run_fb) A.run_fb[f] = (w <= 2 && !exact) ? 1 : 0;
     }
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_draft_bounds (see DraftBoundArgs).  Per raw trough t: the draft value is
+ * r = rolling(W, min_periods, center).quantile(q) at t after bfill/ffill, i.e.
+ * at t clamped to the valid outputs [vfirst, vlast]; with nobs window values,
+ * k = int(q (nobs - 1)) and r in [s_k, s_(k+1)] (= s_k when q (nobs-1) is whole).
+ * Window values lie on segments [t_j, t_(j+1)) of the trough curve (the last
+ * one constant), each monotone between env[t_j] and env[t_(j+1)], so with
+ * lo_j / hi_j the segment's end values and len_j its samples in the window:
+ *   L = min{ lo_j : sum(len_i : lo_i <= lo_j) > k }          -> s_k >= L
+ *   U = min{ hi_j : sum(len_i : hi_i <= hi_j) >= k + 2 (k + 1) } -> s_(k+1) <= U
+ * keep iff env[t] <= mult r: certain when env[t] <= mult L, certainly not
+ * when env[t] > mult U (1 + 2^-50); anything else makes the recording exact. */
+__global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files || !A.run[f]) return;
+    __shared__ int32_t s_tp[DB_TRMAX];
+    __shared__ double s_tv[DB_TRMAX];
+    __shared__ int16_t s_olo[DB_TRMAX], s_ohi[DB_TRMAX];     /* segments by lower / upper end value */
+    __shared__ int s_vf, s_vl, s_undecided;
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    const int m = A.nraw[f];
+    const int tid = threadIdx.x;
+    if (m > DB_TRMAX) {
+        if (tid == 0) A.exact[f] = 1;
+        return;
+    }
+    const int64_t *raw = A.raw + d0;
+    const double *env = A.env + d0;
+    if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; }
+    for (int j = tid; j < m; j += DB_T) {
+        s_tp[j] = (int32_t)raw[j];
+        s_tv[j] = env[raw[j]];
+    }
+    __syncthreads();
+    const int64_t W = A.window, t0 = s_tp[0];
+    auto seg_lo = [&](int j) -> double { return j + 1 < m ? fmin(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
+    auto seg_hi = [&](int j) -> double { return j + 1 < m ? fmax(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
+    /* stable ranks by end value (ties by index): order lists for the walks */
+    for (int j = tid; j < m; j += DB_T) {
+        const double a = seg_lo(j), b = seg_hi(j);
+        int ra = 0, rb = 0;
+        for (int i = 0; i < m; ++i) {
+            const double ai = seg_lo(i), bi = seg_hi(i);
+            ra += (ai < a || (ai == a && i < j)) ? 1 : 0;
+            rb += (bi < b || (bi == b && i < j)) ? 1 : 0;
+        }
+        s_olo[ra] = (int16_t)j;
+        s_ohi[rb] = (int16_t)j;
+    }
+    /* valid outputs (nobs >= min_periods) form one interval */
+    {
+        int vf = INT_MAX, vl = -1;
+        for (int64_t i = tid; i < n; i += DB_T) {
+            int64_t s, e;
+            win_bounds(i, n, W, s, e);
+            const int64_t lo = s > t0 ? s : t0;
+            if (e - lo >= A.min_periods && e > lo) { vf = min(vf, (int)i); vl = max(vl, (int)i); }
+        }
+        for (int o = 32; o > 0; o >>= 1) { vf = min(vf, __shfl_xor(vf, o)); vl = max(vl, __shfl_xor(vl, o)); }
+        if (lane_id() == 0) { atomicMin(&s_vf, vf); atomicMax(&s_vl, vl); }
+    }
+    __syncthreads();
+    const int vf = s_vf, vl = s_vl;
+    if (vl < vf) {                                     /* all-NaN draft: the exact path handles it */
+        if (tid == 0) A.exact[f] = 1;
+        return;
+    }
+    auto seg_of = [&](int64_t x) -> int {           /* last trough <= x (x >= t0) */
+        int lo = 0, hi = m;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= x) lo = mid + 1; else hi = mid; }
+        return lo - 1;
+    };
+    bool any_undecided = false;
+    for (int j = tid; j < m; j += DB_T) {
+        const int64_t t = s_tp[j];
+        const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
+        int64_t s, e;
+        win_bounds(qp, n, W, s, e);
+        const int64_t lo = s > t0 ? s : t0, hi = e, nobs = hi - lo;
+        const double idxf = A.q * (double)(nobs - 1);
+        const int64_t k = (int64_t)idxf;
+        int64_t thr_u = ((double)k == idxf) ? k + 1 : k + 2;
+        if (thr_u > nobs) thr_u = nobs;
+        const int jl = seg_of(lo), jh = seg_of(hi - 1);
+        auto len_of = [&](int i) -> int64_t {          /* samples of segment i inside [lo, hi) */
+            const int64_t a = lo > s_tp[i] ? lo : s_tp[i];
+            const int64_t se = i + 1 < m ? (int64_t)s_tp[i + 1] : n;
+            return (hi < se ? hi : se) - a;
+        };
+        /* L: first lower end (ascending) whose in-window cumulative length exceeds k;
+         * U: first upper end (ascending) whose cumulative reaches thr_u */
+        double L = __builtin_inf(), U = __builtin_inf();
+        int64_t c = 0;
+        for (int r = 0; r < m; ++r) {
+            const int b = s_olo[r];
+            if (b < jl || b > jh) continue;
+            c += len_of(b);
+            if (c > k) { L = seg_lo(b); break; }
+        }
+        c = 0;
+        for (int r = 0; r < m; ++r) {
+            const int b = s_ohi[r];
+            if (b < jl || b > jh) continue;
+            c += len_of(b);
+            if (c >= thr_u) { U = seg_hi(b); break; }
+        }
+        const double et = s_tv[j];
+        uint8_t dcs;
+        if (et <= A.mult * L) dcs = 1;
+        else if (et > A.mult * U * (1.0 + 0x1p-50)) dcs = 0;
+        else { dcs = 2; any_undecided = true; }
+        A.dec[d0 + j] = dcs;
+    }
+    if (any_undecided) s_undecided = 1;
+    __syncthreads();
+    if (tid == 0) A.exact[f] = s_undecided;
 }
 
 __global__ __launch_bounds__(256) void k_floor_final(FinalArgs A) {

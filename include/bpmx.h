@@ -74,8 +74,10 @@ enum bpmx_option {
                                  wavelet-matrix kernel for recordings of <= 20480 decimated samples) */
     BPMX_OPT_NATIVE_F64 = 2,  /* native mode: f64 VALU block projections instead of the exact-integer
                                  matrix-core kernel (test/diagnostic) */
-    BPMX_OPT_HILBERT_ROCFFT = 4 /* native mode: rocFFT R2C/C2R Hilbert instead of the fused in-LDS transform
-                                   (test/diagnostic; recordings the fused kernel cannot plan always use it) */
+    BPMX_OPT_HILBERT_ROCFFT = 4, /* native mode: rocFFT R2C/C2R Hilbert instead of the fused in-LDS transform
+                                    (test/diagnostic; recordings the fused kernel cannot plan always use it) */
+    BPMX_OPT_DRAFT_FULL = 8      /* compute the draft floor (first rolling quantile) in full for every recording
+                                    instead of deciding troughs from its bounds first (test/diagnostic) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

@@ -257,3 +257,19 @@ def test_fused_hilbert_matches_rocfft_and_oracle(det):
         if len(pcm) > 5000 * ds:
             o = O.detect(pcm, fs, params, mode="native")
             _check_file(a, o, exact_env=False)
+
+
+@pytest.mark.parametrize("name", ["ref_44k_60s_mono", "ref_44k_40s_clicks", "vulpine", "env_random_rough",
+                                  "env_plateaus", "env_draft_fallback", "env_random_long_window", "env_static_fallback"])
+def test_draft_bounds_match_full_draft(det, name):
+    """k_draft_bounds (keep decisions from the draft's bracket, the full draft
+    only where one is undecided) gives the golden floor, troughs, flags and
+    peaks, bit for bit, as does computing the draft in full (BPMX_OPT_DRAFT_FULL)."""
+    from bpm_analysis_amd import _native as N
+    g = G.load(name)
+    for opt in (0, N.OPT_DRAFT_FULL):
+        r = det.run_env_host([g["env"]], int(g["sr"]), g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS, options=opt)[0]
+        assert _same(r["floor"], g["floor"])
+        assert _same(r["troughs"], g["troughs"])
+        assert (r["flags"] & 7) == int(g["flags"])
+        assert _same(r["peaks"], g["peaks"])
