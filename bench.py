@@ -45,38 +45,44 @@ def parse():
 
 
 def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, channels: int = 1) -> dict:
-    """Algorithmic HBM bytes per launch of each kernel: the
-    bytes the algorithm must move, not what the implementation happens to move."""
+    """Algorithmic HBM bytes PER STEP of each kernel label (summed over its
+    launches in one step): the bytes the algorithm must
+    move, not what the implementation happens to move."""
     F = n_files
     nb = nd - 1
-    half = nd // 2 + 1
     common = {
         "k_quantile": F * nd * 8,                          # env read once
+        "k_quantile_reg": F * nd * 8,
         "k_block_stats": F * nd * 8,
         "k_find_peaks[troughs]": F * nd * 8,
         "k_find_peaks[peaks]": F * nd * 16,                # env + floor
-        "k_interp": F * nd * 8,                            # dense written once
-        "k_rolling_quantile": F * nd * 16,                 # dense in, quantile out
-        "k_rollq_wm": F * nd * 16,
-        "k_sanitize": 0, "k_floor_final": F * nd * 8,
+        "k_draft_bounds": F * 240 * 16,                    # ~240 raw troughs x (position, value) + decisions
+        # final floor: dense (interpolated in-kernel from the troughs) in, floor out; the
+        # draft pass runs only for recordings with an undecided trough (none on this workload)
+        "k_rollq_wm": F * nd * 8,
+        "k_rolling_quantile": F * nd * 16,
+        "k_floor_final": 0, "k_sanitize": 0, "k_interp": 0,
     }
     if mode == "native":
         return dict(common, **{
             "k_native_blocks": F * n_frames * channels * 2,      # every PCM sample read once (SURVEY 8(d))
             "k_native_carry": F * (nb // 64 * 128 + 64 * 16 * 8),  # tile carries in/out, partial tile
             "k_native_yd": F * nb * (8 + 8),                          # gamma in, yd out
-            "rocfft_r2c": F * (nd * 8 + half * 16),
-            "k_hilbert_rotate": F * half * 16 * 2,
-            "rocfft_c2r": F * (half * 16 + nd * 8),
-            "k_native_env": F * nd * (8 + 8 + 8),
+            "k_hilbert_env": F * nd * (8 + 8),                        # yd in, env out (transform in LDS)
         })
     # reference: the picked samples, y kept in scratch (written fwd, rewritten bwd, read twice), env written once
     return dict(common, **{"k_envelope_ref": F * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8)})
 
 
-def pmc_traffic(mode: str, kernel: str, workload: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (tools/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 calibration), or None."""
+# launch labels -> kernel names in the rocprofv3 PMC summary
+PMC_NAMES = {"k_native_blocks": ("k_native_blocks_mfma", "k_native_blocks_i16", "k_native_blocks_gen"),
+             "k_find_peaks[troughs]": ("k_find_peaks",), "k_find_peaks[peaks]": ("k_find_peaks",)}
+
+
+def pmc_traffic(mode: str, kernel: str, workload: str, launches_per_step: float):
+    """HBM bytes per step of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_traffic.py: mean bytes per dispatch, FETCH_SIZE doubled per the
+    gfx950 calibration) times its launches per step, or None."""
     path = os.path.join(REPO, "profiles", f"pmc_traffic_{mode}.json")
     try:
         with open(path) as fh:
@@ -85,8 +91,11 @@ def pmc_traffic(mode: str, kernel: str, workload: str):
         return None
     if d.get("workload") != workload:
         return None
-    k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+    for name in PMC_NAMES.get(kernel, (kernel,)):
+        k = d.get("kernels", {}).get(name)
+        if k is not None:
+            return int(k["hbm_bytes_per_launch"] * launches_per_step)
+    return None
 
 
 def cpu_baseline(mode: str, fs: int, n_frames: int, n_files: int, params: dict) -> dict:
@@ -219,23 +228,29 @@ def main():
         abytes = algorithmic_bytes(args.mode, F, n, nd, d.ds)
         workload = (f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
                     f"(filter+envelope+noise floor+raw peaks)")
-        # dominant kernel = the largest share of the step (summed over its launches)
+        # dominant kernel = the largest share of the step (summed over its launches);
+        # its roofline point is per step: algorithmic bytes of all its launches in a
+        # step / its time per step (the HIP-event total over the timed steps / steps)
         timed = {k: v for k, v in prof.items() if k in abytes}
         dom = max(timed, key=lambda k: timed[k][1]) if timed else None
         roof = None
         if dom:
             cnt, tot = timed[dom]
-            avg_s = tot / cnt / 1e3
-            ach = abytes[dom] / avg_s / 1e9
+            per_step_s = tot / args.steps / 1e3
+            ach = abytes[dom] / per_step_s / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(args.mode, dom, workload),
-                    "kernel": dom, "kernel_avg_ms": round(avg_s * 1e3, 4),
-                    "algorithmic_bytes_per_launch": abytes[dom]}
+                    "frac": round(ach / HBM_PEAK_GBS, 5),
+                    "traffic": pmc_traffic(args.mode, dom, workload, cnt / args.steps),
+                    "kernel": dom, "kernel_ms_per_step": round(per_step_s * 1e3, 4),
+                    "launches_per_step": cnt / args.steps, "algorithmic_bytes_per_step": abytes[dom]}
         kernels = {}
         for k, (c, t) in sorted(prof.items()):
             kernels[k] = {"launches": c, "avg_ms": round(t / c, 4), "share": round(t / (elapsed * 1e3), 4)}
             if abytes.get(k):
-                kernels[k]["algo_GBps"] = round(abytes[k] / (t / c / 1e3) / 1e9, 1)
+                kernels[k]["algo_GBps"] = round(abytes[k] / (t / args.steps / 1e3) / 1e9, 1)
+                tr = pmc_traffic(args.mode, k, workload, c / args.steps)
+                if tr:
+                    kernels[k]["pmc_bytes_per_step"] = tr
         # whole-step view of the north-star roofline: PCM bytes (read once) / step time
         step_bytes = F * n * 2
         pipeline = {"hbm_bytes_per_step": step_bytes, "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
