@@ -1,5 +1,6 @@
-set -e
-cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_wm -o run -- $GRAFT_REPO_ROOT/tools/kbench 1024 18124 3020 > gpurun_out/pmc_wm.log 2>&1
-timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_wm2 -o run -- $GRAFT_REPO_ROOT/tools/kbench 1024 18124 3020 > gpurun_out/pmc_wm2.log 2>&1
+set -o pipefail
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/pt_all.log 2>&1; rc=$?
+tail -25 gpurun_out/pt_all.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py --no-cpu --pcie-steps 0 > gpurun_out/bench_o0.log 2>&1 || exit 1
+grep "^{" gpurun_out/bench_o0.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], {k:v['avg_ms'] for k,v in d['kernels'].items()})"
