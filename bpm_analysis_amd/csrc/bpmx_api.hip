@@ -301,6 +301,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     bs.env = O->env; bs.doff = d_doff; bs.boff = d_boff; bs.active = d_active; bs.n_files = F;
     bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
     const bool long_files = maxnd > QR_MAX;
+    bool noise_lazy = false;
     if (long_files) LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F), dim3(256), 0, s, bs);
     {
         QuantArgs a;
@@ -311,9 +312,19 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
                 if (a.q[l] == q) { a.slot[l] |= 1 << slot; return; }
             a.q[L] = q; a.slot[L] = 1 << slot; ++L;
         };
-        if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->noise_floor_q, Q_NOISE); add(P->fallback_q, Q_FALLBACK); }
+        /* the noise-floor level (static fallback, < 5 troughs) is computed
+         * lazily after the trough search unless it coincides with a level
+         * needed anyway */
+        if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->fallback_q, Q_FALLBACK); }
         if (do_peaks) add(P->peak_prom_q, Q_PEAK);
+        if (do_floor) {
+            noise_lazy = true;
+            for (int l = 0; l < L; ++l)
+                if (a.q[l] == P->noise_floor_q) { a.slot[l] |= 1 << Q_NOISE; noise_lazy = false; }
+        }
         a.n_levels = L;
+        a.skip = nullptr;
+        a.stats = 1;
         LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
         if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(256), 0, s, a);
     }
@@ -331,6 +342,14 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5;
             LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+        }
+        if (noise_lazy) {                 /* the static-floor quantile, for recordings with < 5 troughs */
+            QuantArgs a;
+            a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
+            a.n_levels = 1; a.q[0] = P->noise_floor_q; a.slot[0] = 1 << Q_NOISE;
+            a.skip = d_run1; a.stats = 0;
+            LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
+            if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, 1), dim3(256), 0, s, a);
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
         const int64_t W = P->noise_window;

@@ -32,6 +32,8 @@ struct QuantArgs {
     double q[Q_SLOTS];
     double *qv;             /* [F][Q_SLOTS] */
     int64_t skip_le;        /* k_quantile: files with n <= skip_le are done by k_quantile_reg */
+    const int32_t *skip;    /* [F] optional: skip files with skip[f] != 0 (the lazy static-floor level) */
+    int32_t stats;          /* k_quantile_reg: also write the block max/min tables */
 };
 
 struct BlockStatArgs {

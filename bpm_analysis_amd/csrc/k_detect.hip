@@ -31,7 +31,7 @@ namespace bpmx {
 /* ------------------------------------------------------------------------ */
 __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
     const int f = blockIdx.x, l = blockIdx.y;
-    if (f >= A.n_files || l >= A.n_levels || !A.active[f]) return;
+    if (f >= A.n_files || l >= A.n_levels || !A.active[f] || (A.skip && A.skip[f])) return;
     const int64_t n = A.doff[f + 1] - A.doff[f];
     if (n <= A.skip_le) return;
     const double *x = A.env + A.doff[f];
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void k_block_stats(BlockStatArgs A) {
  * taken from any key), then the next order statistic and numpy's _lerp. */
 __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArgs B) {
     const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f]) return;
+    if (f >= A.n_files || !A.active[f] || (A.skip && A.skip[f])) return;
     const int64_t n = A.doff[f + 1] - A.doff[f];
     if (n > QR_MAX) return;
     const double *x = A.env + A.doff[f];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArg
         key[it] = ok ? f64_key(v) : 0ull;
         if (ok) { kor |= key[it]; kand &= key[it]; }
         const int64_t b0 = (int64_t)it * QR_T + wid * 64;
-        if (b0 < n) {                                        /* block max/min (k_block_stats) */
+        if (A.stats && b0 < n) {                             /* block max/min (k_block_stats) */
             const double mx = wave_max(ok ? v : -INF), mn = wave_min(ok ? v : INF);
             if (lane == 0) { bmx[b0 >> 6] = mx; bmn[b0 >> 6] = mn; }
         }
