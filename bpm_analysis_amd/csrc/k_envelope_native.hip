@@ -428,11 +428,12 @@ typedef int32_t nm_i16 __attribute__((ext_vector_type(16)));
 
 /* Feeding it: a tile is 64 blocks (~18.7 KB of PCM).  With a tile per wave
  * in flight the chip sits at ~5 TB/s, so tiles travel HBM -> LDS directly by
- * LDS-DMA (global_load_lds_dwordx4, no registers), two slots per wave: the
- * DMA of tile k+2 is issued as soon as the matrix phase of tile k has read its
- * slot, and flies during tile k's epilogue and tile k+1's matrix phase.  Four
- * waves per workgroup, one workgroup per CU: 8 slots + the shared tables fill
- * the 160 KiB LDS. */
+ * LDS-DMA (global_load_lds_dwordx4, no registers), one 18 KB slot per wave:
+ * the DMA of the wave's next tile is issued as soon as the matrix phase has
+ * read the slot and flies during this tile's epilogue.  Four waves per
+ * workgroup, two workgroups per CU: 8 slots (147 KB) + the shared tables fit
+ * the 160 KiB LDS, and with 8 waves interleaving, ~6 of the 8 tiles are in
+ * flight at any time. */
 constexpr int NM_WAVES = 4;
 constexpr int NM_SLOTS = 1;                       /* LDS tile slots per wave */
 constexpr int NM_MINW = 2;                        /* waves per SIMD the register budget must allow */
@@ -478,8 +479,8 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
      * arithmetic below depends on it): chunks past the tile or the batch
      * re-read the batch's last whole chunk into the slot's spare room. */
     const int64_t clast = (total & ~(int64_t)7) - 8;
-    auto dma = [&](int64_t t, u4 *slot) {
-        const int64_t a0 = nat_tile_ld(A.tiles, t).s0 & ~(int64_t)7;
+    auto dma = [&](int64_t s0, u4 *slot) {
+        const int64_t a0 = s0 & ~(int64_t)7;
 #pragma unroll
         for (int r = 0; r < NM_NDMA; ++r) {
             const int q = r * 64 + lane;
@@ -496,10 +497,19 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
     };
     const int64_t stride = (int64_t)gridDim.x * NM_WAVES;
     int64_t t = (int64_t)blockIdx.x * NM_WAVES + wv;
-    if (t < A.n_tiles) dma(t, slots[NM_SLOTS * wv]);
-    if (NM_SLOTS == 2 && t + stride < A.n_tiles) dma(t + stride, slots[NM_SLOTS * wv + 1]);
+    /* Tile headers travel one tile ahead: the next header's scalar load is
+     * issued before this tile's DMA wait, so the refill below never waits on
+     * a header round trip (with one slot per wave that wait would sit between
+     * the slot's read and its next DMA). */
+    NatTile tl{};
+    if (t < A.n_tiles) tl = nat_tile_ld(A.tiles, t);
+    if (t < A.n_tiles) dma(tl.s0, slots[NM_SLOTS * wv]);
+    if (NM_SLOTS == 2 && t + stride < A.n_tiles) dma(nat_tile_ld(A.tiles, t + stride).s0, slots[NM_SLOTS * wv + 1]);
     for (int k = 0; t < A.n_tiles; ++k, t += stride) {
         u4 *slot = slots[NM_SLOTS * wv + (NM_SLOTS == 2 ? (k & 1) : 0)];
+        const int64_t tr = t + NM_SLOTS * stride;               /* the tile this slot is refilled with */
+        NatTile tn{};
+        if (tr < A.n_tiles) tn = nat_tile_ld(A.tiles, tr);
         /* Issued after this tile's DMA: the next tile's NM_NDMA (when there is
          * a next tile) and a few epilogue stores.  vmcnt retires in issue
          * order, so <= NM_NDMA outstanding covers this tile (over-waiting by
@@ -507,7 +517,6 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
          * tile, wait for everything. */
         if (NM_SLOTS == 2 && t + stride < A.n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NM_NDMA) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const NatTile tl = nat_tile_ld(A.tiles, t);
         const int coff = (int)(tl.s0 & 7);
         {
             const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
@@ -560,7 +569,7 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
         /* the slot is read: refill it with the tile after next (two slots) or
          * the next one (one slot: it flies during this epilogue) */
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (t + NM_SLOTS * stride < A.n_tiles) dma(t + NM_SLOTS * stride, slot);
+        if (tr < A.n_tiles) dma(tn.s0, slot);
         /* lane half 0 holds even coefficients, half 1 odd ones; N tile n = blocks 32n.. */
         double cf[8];
 #pragma unroll
@@ -571,6 +580,8 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
         }
         nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{cf[0], cf[1], cf[2], cf[3]}, V4{cf[4], cf[5], cf[6], cf[7]},
                           x0);
+        if (NM_SLOTS == 1) tl = tn;
+        else if (t + stride < A.n_tiles) tl = nat_tile_ld(A.tiles, t + stride);
     }
 }
 template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
