@@ -362,9 +362,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         if (need_merge && (cap > 32 * RQ_T || W + RQ_T >= 65000))
             return fail(BPMX_E_LIMIT, "noise window of " + std::to_string(W) +
                                           " samples exceeds the rolling-quantile kernel (max 7800)");
-        double *wm_sorted = use_wm ? (double *)ctx->buf("wm_sorted", (size_t)sumnd * 8, &rc) : nullptr;
+        uint16_t *wm_pos = use_wm ? (uint16_t *)ctx->buf("wm_pos", (size_t)sumnd * 2, &rc) : nullptr;   /* rank -> index */
+        int32_t *wm_full = use_wm ? (int32_t *)ctx->buf("wm_full", (size_t)F * 4, &rc) : nullptr;
         if (rc != BPMX_OK) return rc;
-        const size_t wm_lds = wm_lds_bytes(std::min<int64_t>(maxnd, WM_MMAX));
+        const int64_t wm_n = std::min<int64_t>(maxnd, WM_MMAX);
+        const size_t wm_lds_p = wm_layout(wm_n, true).total, wm_lds = wm_layout(wm_n, false).total;
         auto rollq = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, double *outp,
                          int32_t *allnan) -> int {
             RollqArgs a;
@@ -373,9 +375,21 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
             a.out = outp; a.allnan = allnan; a.wm_max = use_wm ? WM_MMAX : 0;
             if (use_wm) {
-                (void)hipFuncSetAttribute((const void *)k_rollq_wm, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)wm_lds);
-                LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm, dim3(F), dim3(WM_T), wm_lds, s, a, wm_sorted);
+                /* pruned structure first; recordings it cannot take (too many
+                 * kept samples, > WM_TRMAX troughs) are flagged in wm_full for
+                 * the unpruned variant */
+                RollqArgs b = a;
+                if (!(P->options & BPMX_OPT_ROLLQ_NOPRUNE)) {
+                    (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds_p);
+                    LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F), dim3(WM_T), wm_lds_p, s, a, wm_pos,
+                           wm_full);
+                    b.run = wm_full;
+                }
+                (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds);
+                LAUNCH(ctx, s, "k_rollq_wm[full]", k_rollq_wm_t<false>, dim3(F), dim3(WM_T), wm_lds, s, b, wm_pos,
+                       wm_full);
             }
             if (!need_merge) return BPMX_OK;
             if (cap <= 16 * RQ_T) {

@@ -131,6 +131,32 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
+/* wave64 inclusive scan (sum, or running max) in registers with DPP: row
+ * shifts 1/2/4/8 scan each 16-lane row, row_bcast:15 / row_bcast:31 carry the
+ * row totals forward (GFX9 DPP; no LDS round trip, unlike __shfl_up).  Every
+ * lane of the wave must be active. */
+template <bool MAX>
+__device__ __forceinline__ int wave_iscan_dpp(int x) {
+    const int id = MAX ? INT_MIN : 0;
+#define BPMX_DPP_STEP(ctrl, rmask)                                              \
+    {                                                                           \
+        const int t = __builtin_amdgcn_update_dpp(id, x, ctrl, rmask, 0xf, false); \
+        x = MAX ? (t > x ? t : x) : x + t;                                      \
+    }
+    BPMX_DPP_STEP(0x111, 0xf)   /* row_shr:1 */
+    BPMX_DPP_STEP(0x112, 0xf)   /* row_shr:2 */
+    BPMX_DPP_STEP(0x114, 0xf)   /* row_shr:4 */
+    BPMX_DPP_STEP(0x118, 0xf)   /* row_shr:8 */
+    BPMX_DPP_STEP(0x142, 0xa)   /* row_bcast:15 -> rows 1, 3 */
+    BPMX_DPP_STEP(0x143, 0xc)   /* row_bcast:31 -> rows 2, 3 */
+#undef BPMX_DPP_STEP
+    return x;
+}
+/* value of the lane below (lane 0 gets `edge`) */
+__device__ __forceinline__ int wave_shr1_dpp(int x, int edge) {
+    return __builtin_amdgcn_update_dpp(edge, x, 0x138, 0xf, 0xf, false);   /* wave_shr:1 */
+}
+
 /* exclusive block scan of 0/1 flags; `sh` holds NT/64+1 ints.  Returns the
  * exclusive prefix, writes the block total to *total.  Ends with a barrier. */
 template <int NT>

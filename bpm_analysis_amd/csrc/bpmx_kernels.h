@@ -178,17 +178,35 @@ constexpr int WM_T = 1024;
 constexpr int WM_ITEMS = 18;                 /* 16-bit positions; LDS ~156 KB at the maximum */
 constexpr int WM_MMAX = WM_T * WM_ITEMS;     /* 18432 decimated samples (61 s at 302 Hz) */
 constexpr int WM_TRMAX = 512;                /* troughs staged in LDS for the in-kernel interpolation */
-__host__ __device__ inline size_t wm_lds_bytes(int64_t nmax) {
-    const int64_t m = nmax < 1 ? 1 : nmax;
+constexpr int WM_PMAX = 12288;               /* kept samples of the pruned variant */
+/* dynamic LDS of k_rollq_wm_t: trough tables | (pruned) kept masks, prefix,
+ * bins | (pruned) kept positions | phase area (histogram / sort / matrix) */
+struct WmLayout {
+    size_t tab, meta, kpos, area, total;
+};
+__host__ __device__ inline size_t wm_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline WmLayout wm_layout(int64_t nmax, bool prune) {
+    const int64_t n = nmax < 1 ? 1 : (nmax > WM_MMAX ? WM_MMAX : nmax);
+    const int64_t m = prune && n > WM_PMAX ? WM_PMAX : n;
     const int64_t L = m > 1 ? 64 - __builtin_clzll((unsigned long long)(m - 1)) : 1;
     const int64_t NW = (m + 63) / 64;
     const int64_t m8 = (m + 7) & ~7LL;
+    const int64_t NBK = WM_MMAX / 64 + 2;                              /* per-64 tables */
     const int64_t sort_b = 8 * m8 + (int64_t)(WM_T / 64) * 128 * 4;   /* pos x2, key halves, counters */
-    /* + troughs (WM_TRMAX * 12 B) and their per-64-block index, after the larger phase */
     const int64_t wm_b = 4 * m8 + L * (2 * NW + 1) * 8;               /* sequences x2, levels */
-    return (size_t)(sort_b > wm_b ? sort_b : wm_b) + (size_t)WM_TRMAX * 12 + (size_t)(m / 64 + 2) * 4;
+    const int64_t hist_b = prune ? NBK * 64 * 2 + (int64_t)(WM_T / 64) * 64 * 4 + n : 0;   /* + bin per sample */
+    int64_t area = sort_b > wm_b ? sort_b : wm_b;
+    area = area > hist_b ? area : hist_b;
+    WmLayout l;
+    l.tab = 0;
+    l.meta = wm_align16((size_t)WM_TRMAX * (prune ? 20 : 12) + (size_t)NBK * 4);
+    l.kpos = wm_align16(l.meta + (prune ? (size_t)NBK * 22 : 0));   /* mask 8, prefix 4, thr 1, b* levels 9 */
+    l.area = wm_align16(l.kpos + (prune ? (size_t)m * 2 : 0));
+    l.total = l.area + (size_t)area;
+    return l;
 }
-__global__ void k_rollq_wm(RollqArgs A, double *sorted_scratch);
+template <bool PRUNE>
+__global__ void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full);
 
 }  // namespace bpmx
 

@@ -9,7 +9,7 @@
 /* Optional in-kernel phase timing (tools/kbench.hip builds with -DBPMX_STAMPS;
  * the library never does): thread 0 accumulates s_memtime deltas per phase. */
 #ifdef BPMX_STAMPS
-#define STAMP_DECL unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _st_t = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL unsigned long long _st_acc[16] = {0}, _st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(k)                                                                  \
     do {                                                                          \
         if (threadIdx.x == 0) {                                                   \
@@ -21,7 +21,7 @@
 #define STAMP_FLUSH(ptr)                                                          \
     do {                                                                          \
         if (threadIdx.x == 0 && (ptr))                                            \
-            for (int _k = 0; _k < 8; ++_k) (ptr)[blockIdx.x * 8 + _k] = _st_acc[_k]; \
+            for (int _k = 0; _k < 16; ++_k) (ptr)[blockIdx.x * 16 + _k] = _st_acc[_k]; \
     } while (0)
 #else
 #define STAMP_DECL

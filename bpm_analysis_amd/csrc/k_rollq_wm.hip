@@ -4,21 +4,33 @@
  *  .rolling(W, min_periods=3, center=True).quantile(q).bfill().ffill()).
  *
  * One 1024-thread workgroup per recording, everything in LDS:
- *   1. ranks: the finite suffix dense[t0:n) is ordered by (value, position)
- *      with an LSD radix sort on order-preserving 64-bit keys, 8-bit digits,
- *      digits constant over the recording skipped.  What moves is only the
- *      16-bit position (ping-pong in LDS); the current 32-bit key half sits
- *      in LDS indexed by position (low halves for digits 0-3, then high
- *      halves).  Slots are wave-contiguous, so a stable rank is: per-wave
- *      digit counter (LDS atomic, issued in slot order) + peers below in the
- *      same round (ballot match) + one (digit, wave) block scan.
+ *   0. (pruned variant) only samples that can be some window's k-th or
+ *      (k+1)-th smallest enter the structure.  Values are put in 64 monotone
+ *      bins; per block of 64 outputs, the bin b* holding the (k_max+1)-th
+ *      smallest sample of the block's common window (the intersection of its
+ *      64 windows, full 64-sample position blocks only) bounds every one of
+ *      its windows' (k+1)-th smallest from above.  A sample whose bin exceeds
+ *      b* of every block whose windows can contain it is strictly greater than
+ *      each such window's (k+1)-th smallest, so dropping it changes no output;
+ *      the window's k-th smallest is the k-th smallest of its kept samples.
+ *      Kept samples are compacted (a per-64 bit mask + prefix maps a position
+ *      range to a kept range).  On the metric workload ~30 % are kept.
+ *      Recordings keeping more than WM_PMAX take the unpruned variant.
+ *   1. ranks: the kept samples are ordered by (value, index) with an LSD radix
+ *      sort on order-preserving 64-bit keys, 8-bit digits, digits constant
+ *      over the recording skipped.  What moves is only the 16-bit index
+ *      (ping-pong in LDS); the current 32-bit key half sits in LDS indexed by
+ *      index (low halves for digits 0-3, then high halves).  Slots are
+ *      wave-contiguous, so a stable rank is: per-wave digit counter (LDS
+ *      atomic, issued in slot order) + peers below in the same round (ballot
+ *      match) + one (digit, wave) block scan.
  *   2. wavelet matrix over the rank sequence (ceil(log2 m) levels): per level
- *      a bit vector with a rank directory, {word, ones-before} in 16 B.
- *   3. every output independently: its window's k-th and (k+1)-th smallest by
- *      two interleaved top-down descents (O(log m) LDS reads each), pandas'
- *      linear interpolation, nobs / min_periods from the window bounds.  NaN
- *      outputs are a prefix and a suffix (nobs is unimodal), filled from the
- *      first and last valid output.
+ *      a bit vector with a rank directory, {word, ones-before} per 32 samples.
+ *   3. every output independently: its window's k-th smallest by one top-down
+ *      descent, the (k+1)-th by walking up the rank order to the next rank
+ *      inside the window; pandas' linear interpolation, nobs / min_periods
+ *      from the window bounds.  NaN outputs are a prefix and a suffix (nobs is
+ *      unimodal), filled from the first and last valid output.
  * Recordings longer than WM_MMAX decimated samples take k_rolling_quantile.
  */
 #include "bpmx_common.h"
@@ -52,43 +64,45 @@ struct WmRec {
     uint32_t ones;
 };
 
-__global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_scratch) {
+template <bool PRUNE>
+__global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full) {
     constexpr int NWV = WM_T / 64;
-    constexpr int MAXIT = WM_MMAX / WM_T;
+    constexpr int MMAX = PRUNE ? WM_PMAX : WM_MMAX;          /* samples in the structure */
+    constexpr int MAXIT = MMAX / WM_T;
     const int f = blockIdx.x;
-    if (f >= A.n_files || !A.run[f]) return;
-    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
-    if (n > WM_MMAX || n <= 0) return;                       /* k_rolling_quantile handles it */
-    extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_first, s_last, s_Z[16], s_wt[NWV];
-    __shared__ unsigned long long s_or[NWV], s_and[NWV];
-
+    if (f >= A.n_files) return;
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+    if (!A.run[f]) {
+        if (PRUNE && tid == 0) full[f] = 0;
+        return;
+    }
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    const int ntr = A.env ? A.ntr[f] : 0;
+    const bool fused = A.env && ntr <= WM_TRMAX;
+    if (n > WM_MMAX || n <= 0 || (PRUNE && !fused)) {        /* k_rolling_quantile / the unpruned variant */
+        if (PRUNE && tid == 0) full[f] = (n <= WM_MMAX && n > 0) ? 1 : 0;
+        return;
+    }
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_first, s_last, s_Z[16], s_wt[NWV], s_mk;
+    __shared__ unsigned long long s_or[NWV], s_and[NWV];
+    __shared__ double s_vmin, s_vmax;
+
     const double *dense = A.dense + d0;
     double *out = A.out + d0;
-    double *sv = sorted_scratch + d0;                        /* sorted values, rank order */
+    uint16_t *ps = pos_scratch + d0;                         /* kept index of each rank */
     const int64_t t0 = A.troughs[d0];
-    const int m = (int)(n - t0);                             /* finite samples dense[t0:n) */
-    const int IT = (m + WM_T - 1) / WM_T;                    /* rounds per wave */
-    const int S = 64 * IT;                                   /* slots per wave */
+    const int mall = (int)(n - t0);                          /* finite samples dense[t0:n) */
+    const WmLayout Lay = wm_layout(n, PRUNE);
     if (tid == 0) { s_first = INT_MAX; s_last = -1; }
     STAMP_DECL
 
     /* dense = np.interp of the troughs (k_interp), evaluated here from env at
      * the troughs staged in LDS when there are <= WM_TRMAX of them */
-    const int ntr = A.env ? A.ntr[f] : 0;
-    const bool fused = A.env && ntr <= WM_TRMAX;
-    int32_t *s_tp, *s_bj;
-    double *s_tv;
-    {
-        const int64_t n8 = (n + 7) & ~7LL;
-        const int64_t Ln = n > 1 ? 64 - __builtin_clzll((unsigned long long)(n - 1)) : 1;
-        const int64_t sort_b = 8 * n8 + (int64_t)NWV * 128 * 4;
-        const int64_t wm_b = 4 * n8 + Ln * (2 * ((n + 63) / 64) + 1) * 8;
-        s_tv = (double *)(smem + (sort_b > wm_b ? sort_b : wm_b));
-        s_tp = (int32_t *)(s_tv + WM_TRMAX);
-        s_bj = s_tp + WM_TRMAX;                              /* [n/64 + 1]: last trough <= block start */
-    }
+    double *s_tv = (double *)(smem + Lay.tab);
+    double *s_sl = s_tv + WM_TRMAX;                          /* per-segment slope (pruned variant) */
+    int32_t *s_tp = (int32_t *)(s_sl + (PRUNE ? WM_TRMAX : 0));
+    int32_t *s_bj = s_tp + WM_TRMAX;                         /* [n/64 + 1]: last trough <= block start */
     if (fused) {
         const int64_t *tr = A.troughs + d0;
         for (int j = tid; j < ntr; j += WM_T) {
@@ -101,6 +115,11 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
             while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= (b << 6)) lo = mid + 1; else hi = mid; }
             s_bj[b] = lo - 1;
         }
+        if (PRUNE) {
+            /* the same slope interp_at computes, once per segment */
+            for (int j = tid; j + 1 < ntr; j += WM_T)
+                s_sl[j] = (s_tv[j + 1] - s_tv[j]) / ((double)s_tp[j + 1] - (double)s_tp[j]);
+        }
         __syncthreads();
     }
     /* interp_at's arithmetic, with the bracketing trough found from the block table */
@@ -112,7 +131,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
         while (j + 1 < ntr && s_tp[j + 1] <= x) ++j;
         if (j == ntr - 1 || s_tp[j] == x) return s_tv[j];
         const double y0 = s_tv[j], y1 = s_tv[j + 1];
-        const double slope = (y1 - y0) / ((double)s_tp[j + 1] - (double)s_tp[j]);
+        const double slope = PRUNE ? s_sl[j] : (y1 - y0) / ((double)s_tp[j + 1] - (double)s_tp[j]);
         double r = slope * ((double)x - (double)s_tp[j]) + y0;
         if (r != r) {
             r = slope * ((double)x - (double)s_tp[j + 1]) + y1;
@@ -121,10 +140,212 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
         return r;
     };
 
+    const int64_t W = A.window, minp = A.min_periods;
+    const double q = A.q;
+
+    /* ---------------- 0. pruning (PRUNE only) ---------------- */
+    const int NPB = (mall + 63) >> 6;                        /* 64-sample position blocks of dense[t0:n) */
+    uint64_t *kmask = (uint64_t *)(smem + Lay.meta);         /* [NPB + 1] kept bits */
+    int32_t *kpre = (int32_t *)(kmask + (WM_MMAX / 64 + 2)); /* [NPB + 1] kept before the block */
+    uint8_t *thr = (uint8_t *)(kpre + (WM_MMAX / 64 + 2));   /* [NPB] highest bin kept */
+    uint8_t *bstar = thr + (WM_MMAX / 64 + 2);               /* [9][n/64] per output block, then sparse-table maxima */
+    uint16_t *kpos = (uint16_t *)(smem + Lay.kpos);          /* kept index -> position - t0 */
+    int m = mall;
+    if (PRUNE) {
+        constexpr int NB = 64;
+        STAMP(8);
+        /* value range of the curve = range of the trough values (interpolation
+         * stays between segment ends up to rounding; the bins clamp) */
+        {
+            double lo = __builtin_inf(), hi = -__builtin_inf();
+            for (int j = tid; j < ntr; j += WM_T) { lo = fmin(lo, s_tv[j]); hi = fmax(hi, s_tv[j]); }
+            lo = wave_min(lo);
+            hi = wave_max(hi);
+            if (lane == 0) { s_or[wid] = (unsigned long long)__double_as_longlong(lo); s_and[wid] = (unsigned long long)__double_as_longlong(hi); }
+            __syncthreads();
+            if (tid == 0) {
+                for (int w = 0; w < NWV; ++w) {
+                    lo = fmin(lo, __longlong_as_double((long long)s_or[w]));
+                    hi = fmax(hi, __longlong_as_double((long long)s_and[w]));
+                }
+                s_vmin = lo;
+                s_vmax = hi;
+            }
+        }
+        uint16_t *hist = (uint16_t *)(smem + Lay.area);      /* [NPB + 1][NB], then the exclusive prefix over blocks */
+        int32_t *hsc = (int32_t *)(hist + (WM_MMAX / 64 + 2) * NB);   /* [NWV][NB] */
+        for (int j = tid; j < (NPB + 1) * NB / 2; j += WM_T) ((uint32_t *)hist)[j] = 0u;
+        __syncthreads();
+        const double vmin = s_vmin, span = s_vmax - s_vmin;
+        const bool ok = span == span && span < __builtin_inf();
+        if (!ok) {                                           /* non-finite curve: no pruning */
+            if (tid == 0) full[f] = 1;
+            return;
+        }
+        const double scale = span > 0.0 ? (double)NB / span : 0.0;
+        /* monotone in the value: (v - vmin) * scale rounds monotonically, the
+         * truncation and the clamp are monotone */
+        auto vbin = [&](double v) -> int {
+            const double t = (v - vmin) * scale;
+            int b = t > 0.0 ? (int)fmin(t, (double)(NB - 1)) : 0;
+            return b;
+        };
+        uint8_t *bin8 = (uint8_t *)(hsc + NWV * NB);        /* [mall] bin of each sample */
+        /* one 64-sample block per wave step: runs of equal bins (the curve is
+         * piecewise monotone, so a block has few) each add their length */
+        for (int p0 = wid << 6; p0 < mall; p0 += WM_T) {
+            const int p = p0 + lane, nv = min(64, mall - p0);
+            const int b = p < mall ? vbin(dval(t0 + p)) : -1;
+            if (p < mall) bin8[p] = (uint8_t)b;
+            const int bprev = wave_shr1_dpp(b, -1);          /* all lanes active here */
+            const bool start = b >= 0 && (lane == 0 || bprev != b);
+            const uint64_t sm = __ballot(start);
+            const uint64_t after = sm & ~((2ull << lane) - 1ull);
+            const int nxt = after ? __ffsll((long long)after) - 1 : nv;
+            if (start) atomicAdd((uint32_t *)hist + (((p0 >> 6) * NB + b) >> 1), (uint32_t)(nxt - lane) << (16 * (b & 1)));
+        }
+        __syncthreads();
+        STAMP(9);
+        /* exclusive prefix over position blocks, per bin: 16 parts of rows */
+        {
+            const int b = tid & (NB - 1), g = tid >> 6;
+            constexpr int RPMAX = (WM_MMAX / 64 + 1 + NWV - 1) / NWV;
+            const int rp = (NPB + NWV - 1) / NWV, r0 = g * rp, r1 = min(NPB, r0 + rp);
+            int hv[RPMAX], sum = 0;
+#pragma unroll
+            for (int u = 0; u < RPMAX; ++u) {
+                hv[u] = r0 + u < r1 ? (int)hist[(r0 + u) * NB + b] : 0;
+                sum += hv[u];
+            }
+            hsc[g * NB + b] = sum;
+            __syncthreads();
+            int run = 0;
+            for (int h = 0; h < g; ++h) run += hsc[h * NB + b];
+#pragma unroll
+            for (int u = 0; u < RPMAX; ++u) {
+                if (r0 + u < r1) hist[(r0 + u) * NB + b] = (uint16_t)run;
+                run += hv[u];
+            }
+            if (g == NWV - 1) {
+                int tot = 0;
+                for (int h = 0; h < NWV; ++h) tot += hsc[h * NB + b];
+                hist[NPB * NB + b] = (uint16_t)tot;
+            }
+        }
+        __syncthreads();
+        STAMP(10);
+        /* cumulative over bins too: hist[r][b] = samples of blocks < r with bin <= b */
+        for (int r = wid; r <= NPB; r += NWV) {
+            const int v = wave_iscan_dpp<false>((int)hist[r * NB + lane]);
+            hist[r * NB + lane] = (uint16_t)v;
+        }
+        __syncthreads();
+        /* b* per block of 64 outputs, one thread per block: the lowest bin
+         * with >= k_max + 2 samples of the block's common window (full
+         * position blocks only) at or below it, by binary search */
+        const int NBO = (int)((n + 63) >> 6);
+        for (int B = tid; B < NBO; B += WM_T) {
+            const int64_t ib = (int64_t)B << 6, ie = min<int64_t>(n, ib + 64) - 1;
+            int64_t s0, e0, s1, e1;
+            win_bounds(ib, n, W, s0, e0);
+            win_bounds(ie, n, W, s1, e1);
+            /* every window of the block holds <= min(W, e(ie) - max(s(ib), t0)) samples */
+            int64_t nb = e1 - (s0 > t0 ? s0 : t0);
+            nb = nb < W ? nb : W;
+            const int kq = nb > 1 ? (int)(int64_t)(q * (double)(nb - 1)) : 0;
+            const int64_t clo = (s1 > t0 ? s1 : t0) - t0, chi = e0 - t0;   /* common window, relative */
+            const int pbs = (int)((clo + 63) >> 6), pbe = chi > 0 ? (int)(chi >> 6) : 0;
+            int bs = NB - 1;
+            if (pbe > pbs && (int)hist[pbe * NB + NB - 1] - (int)hist[pbs * NB + NB - 1] >= kq + 2) {
+                int lo = 0, hi = NB - 1;                     /* count(<= hi) reaches */
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if ((int)hist[pbe * NB + mid] - (int)hist[pbs * NB + mid] >= kq + 2) hi = mid; else lo = mid + 1;
+                }
+                bs = lo;
+            }
+            bstar[B] = (uint8_t)bs;
+        }
+        __syncthreads();
+        /* sparse table of b* maxima over 2^j consecutive blocks, j = 1 .. 8 */
+        for (int j = 1; (1 << j) <= NBO; ++j) {
+            const uint8_t *src = bstar + (size_t)(j - 1) * (WM_MMAX / 64 + 2);
+            uint8_t *dst = bstar + (size_t)j * (WM_MMAX / 64 + 2);
+            for (int B = tid; B + (1 << j) <= NBO; B += WM_T) dst[B] = max(src[B], src[B + (1 << (j - 1))]);
+            __syncthreads();
+        }
+        STAMP(11);
+        /* highest b* over the output blocks whose windows can reach a position block */
+        const int64_t off = (W - 1) / 2;
+        for (int pb = tid; pb < NPB; pb += WM_T) {
+            const int64_t a = t0 + ((int64_t)pb << 6);
+            const int64_t ilo = a - off > 0 ? a - off : 0;
+            int64_t ihi = min<int64_t>(n - 1, a + 63 + W - off);
+            if (ihi >= n - 1 - off) ihi = n - 1;             /* windows clamped at n are all alike */
+            const int B0 = (int)(ilo >> 6), B1 = (int)(ihi >> 6), len = B1 - B0 + 1;
+            const int j = 31 - __clz(len);
+            const uint8_t *st = bstar + (size_t)j * (WM_MMAX / 64 + 2);
+            thr[pb] = max(st[B0], st[B1 - (1 << j) + 1]);
+        }
+        __syncthreads();
+        STAMP(12);
+        /* keep masks, one 64-sample block per wave step */
+        int kc = 0;
+        for (int pb = wid; pb < NPB; pb += NWV) {
+            const int p = (pb << 6) + lane;
+            const bool keep = p < mall && (int)bin8[p] <= (int)thr[pb];
+            const uint64_t bal = __ballot(keep);
+            if (lane == 0) kmask[pb] = bal;
+        }
+        if (tid == 0) kmask[NPB] = 0ull;
+        __syncthreads();
+        /* exclusive prefix of kept counts over blocks (NPB <= 289: one wave) */
+        if (wid == 0) {
+            int run = 0;
+            for (int base = 0; base < NPB; base += 64) {
+                const int pb = base + lane;
+                const int v = pb < NPB ? __popcll(kmask[pb]) : 0;
+                int x = v;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
+                }
+                if (pb < NPB) kpre[pb] = run + x - v;
+                run += __shfl(x, 63);
+            }
+            if (lane == 0) { kpre[NPB] = run; s_mk = run; }
+        }
+        __syncthreads();
+        kc = s_mk;
+        STAMP(13);
+        if (kc > WM_PMAX) {                                  /* too many kept: the unpruned variant */
+            if (tid == 0) full[f] = 1;
+            return;
+        }
+        if (tid == 0) full[f] = 0;
+        for (int pb = wid; pb < NPB; pb += NWV) {
+            const uint64_t mk = kmask[pb];
+            if ((mk >> lane) & 1) kpos[kpre[pb] + __popcll(mk & lanemask_lt())] = (uint16_t)((pb << 6) + lane);
+        }
+        m = kc;
+        __syncthreads();
+    }
+    /* relative position of the c-th sample in the structure */
+    auto spos = [&](int c) -> int { return PRUNE ? (int)kpos[c] : c; };
+    /* structure index range of relative positions [0, p) */
+    auto kidx = [&](int p) -> int {
+        if (!PRUNE) return p;
+        const uint64_t mk = kmask[p >> 6];
+        return kpre[p >> 6] + __popcll(mk & ((1ull << (p & 63)) - 1ull));
+    };
+    STAMP(7);
+
     /* LDS, sort phase: posA[m8] | posB[m8] | kh[m8] | cnt[NWV][128] (two 16-bit counters per word).
      * Slots >= m are padding: they sort last, so they are neither stored nor counted. */
+    const int IT = (m + WM_T - 1) / WM_T;                    /* rounds per wave */
+    const int S = 64 * IT;                                   /* slots per wave */
     const int m8 = (m + 7) & ~7;
-    uint16_t *posA = (uint16_t *)smem;
+    uint16_t *posA = (uint16_t *)(smem + Lay.area);
     uint16_t *posB = posA + m8;
     uint32_t *kh = (uint32_t *)(posB + m8);
     uint32_t *cnt = kh + m8;
@@ -132,8 +353,8 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     /* ---------------- 1. ranks by LSD radix sort ---------------- */
     uint64_t kor = 0, kand = ~0ull;
     for (int p = tid; p < m; p += WM_T) {
-        posA[p] = (uint16_t)p;                               /* slot order == position order */
-        const uint64_t k = wm_key(dval(t0 + p));
+        posA[p] = (uint16_t)p;                               /* slot order == index order */
+        const uint64_t k = wm_key(dval(t0 + spos(p)));
         kh[p] = (uint32_t)k;
         kor |= k;
         kand &= k;
@@ -153,8 +374,8 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     STAMP(0);
     uint32_t *wc = cnt + wid * 128;
     for (int d = 0; d < 8; ++d) {
-        if (d == 4 && (vary >> 32)) {                        /* high halves, indexed by position */
-            for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(wm_key(dval(t0 + p)) >> 32);
+        if (d == 4 && (vary >> 32)) {                        /* high halves, indexed by index */
+            for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(wm_key(dval(t0 + spos(p))) >> 32);
             __syncthreads();
         }
         if (((vary >> (8 * d)) & 0xFFull) == 0) continue;    /* uniform: constant digit, order unchanged */
@@ -232,7 +453,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
         uint16_t *t = posA; posA = posB; posB = t;
         STAMP(3);
     }
-    /* posA[r] = position of rank r.  Build: seqA = the free pos buffer,
+    /* posA[r] = index of rank r.  Build: seqA = the free pos buffer,
      * seqB = posA once consumed; levels over the dead kh / cnt. */
     const int L = m > 1 ? 32 - __clz(m - 1) : 1;              /* levels: ranks < 2^L */
     const int NW = (m + 63) >> 6;                             /* 64-bit words per level */
@@ -241,23 +462,30 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     WmRec *lv = (WmRec *)kh;                                  /* [L][NR] */
     for (int r = tid; r < m; r += WM_T) {
         const int p = posA[r];
-        sv[r] = dval(t0 + p);
+        ps[r] = (uint16_t)p;
         seqA[p] = (uint16_t)r;
     }
     __syncthreads();
     STAMP(4);
 
     /* ---------------- 2. wavelet matrix ---------------- */
-    const int cw = (NW + NWV - 1) / NWV;                     /* words per wave (<= 64) */
-    const int wb = wid * cw, we = min(NW, wb + cw);
+    constexpr int CWMAX = (MMAX / 64 + NWV - 1) / NWV;       /* words per wave at the maximum */
+    const int cw = (NW + NWV - 1) / NWV;                     /* words per wave (<= CWMAX) */
+    const int wb = wid * cw, nwv = max(0, min(NW, wb + cw) - wb);
     for (int l = L - 1; l >= 0; --l) {
         WmRec *row = lv + l * NR;
-        /* ones among this wave's words (ballots are wave-uniform: scalar sums) */
+        /* this wave's words into registers first (independent LDS reads), then
+         * ones among them (ballots are wave-uniform: scalar sums) */
+        uint32_t sq[CWMAX];
         uint32_t wones = 0;
-        for (int w = wb; w < we; ++w) {
-            const int p = w * 64 + lane;
-            wones += (uint32_t)__popcll(__ballot(p < m && ((seqA[p] >> l) & 1)));
+#pragma unroll
+        for (int w = 0; w < CWMAX; ++w) {
+            const int p = (wb + w) * 64 + lane;
+            sq[w] = (w < nwv && p < m) ? (uint32_t)seqA[p] : 0xFFFFFFFFu;   /* all-ones: invalid */
         }
+#pragma unroll
+        for (int w = 0; w < CWMAX; ++w)
+            wones += (uint32_t)__popcll(__ballot(sq[w] != 0xFFFFFFFFu && ((sq[w] >> l) & 1)));
         if (lane == 0) s_wt[wid] = (int)wones;
         __syncthreads();
         uint32_t run = 0, tot = 0;
@@ -272,47 +500,58 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
             s_Z[l] = Z;
         }
         /* stable partition (zeros, then ones) and the rank directory */
-        for (int w = wb; w < we; ++w) {
-            const int p = w * 64 + lane;
-            const uint32_t v = p < m ? seqA[p] : 0u;
-            const bool bit = p < m && ((v >> l) & 1);
-            const uint64_t word = __ballot(bit);
-            if (lane == 0) {
-                row[2 * w] = WmRec{(uint32_t)word, run};
-                row[2 * w + 1] = WmRec{(uint32_t)(word >> 32), run + (uint32_t)__popc((uint32_t)word)};
+#pragma unroll
+        for (int w = 0; w < CWMAX; ++w) {
+            if (w < nwv) {
+                const int p = (wb + w) * 64 + lane;
+                const bool bit = sq[w] != 0xFFFFFFFFu && ((sq[w] >> l) & 1);
+                const uint64_t word = __ballot(bit);
+                if (lane == 0) {
+                    row[2 * (wb + w)] = WmRec{(uint32_t)word, run};
+                    row[2 * (wb + w) + 1] = WmRec{(uint32_t)(word >> 32), run + (uint32_t)__popc((uint32_t)word)};
+                }
+                const int o1 = (int)run + __popcll(word & lanemask_lt());
+                if (sq[w] != 0xFFFFFFFFu) seqB[bit ? Z + o1 : p - o1] = (uint16_t)sq[w];
+                run += (uint32_t)__popcll(word);
             }
-            const int o1 = (int)run + __popcll(word & lanemask_lt());
-            if (p < m) seqB[bit ? Z + o1 : p - o1] = (uint16_t)v;
-            run += (uint32_t)__popcll(word);
         }
         __syncthreads();
         uint16_t *t = seqA; seqA = seqB; seqB = t;
     }
+    /* rank -> index back into LDS over the dead sequence buffer */
     __threadfence_block();
+    uint16_t *posR = seqA;
+    for (int r = tid; r < m; r += WM_T) posR[r] = ps[r];
+    /* sorted values in LDS past the levels when they fit (pruned variant);
+     * otherwise each output evaluates its two values from the troughs */
+    double *svl = nullptr;
+    if (PRUNE) {
+        const size_t off = ((size_t)4 * m8 + (size_t)L * NR * 8 + 15) & ~(size_t)15;
+        if (off + (size_t)8 * m <= Lay.total - Lay.area) svl = (double *)(smem + Lay.area + off);
+    }
+    __syncthreads();
+    if (svl) {
+        for (int r = tid; r < m; r += WM_T) svl[r] = dval(t0 + spos(posR[r]));
+        __syncthreads();
+    }
     STAMP(5);
 
     /* ---------------- 3. outputs ---------------- */
-    const int64_t W = A.window, minp = A.min_periods;
-    const double q = A.q;
     auto rk = [&](const WmRec *row, int i) {
         const WmRec r = row[i >> 5];
         return (int)r.ones + __popc(r.word & ((1u << (i & 31)) - 1u));
     };
-    /* k-th and (k+1)-th smallest of positions [lo, hi): two interleaved descents */
-    auto kth2 = [&](int lo, int hi, int k, int &ra, int &rb) {
-        int la = lo, ha = hi, ka = k, lb = lo, hb = hi, kb = k + 1;
-        ra = 0;
-        rb = 0;
+    /* the k-th smallest of structure indices [lo, hi): one top-down descent */
+    auto kth = [&](int lo, int hi, int k) {
+        int r = 0;
         for (int l = L - 1; l >= 0; --l) {
             const WmRec *row = lv + l * NR;
-            const int oa0 = rk(row, la), oa1 = rk(row, ha), ob0 = rk(row, lb), ob1 = rk(row, hb);
-            const int Z = s_Z[l];
-            const int za = (ha - oa1) - (la - oa0), zb = (hb - ob1) - (lb - ob0);
-            if (ka < za) { la -= oa0; ha -= oa1; }
-            else { ka -= za; la = Z + oa0; ha = Z + oa1; ra |= 1 << l; }
-            if (kb < zb) { lb -= ob0; hb -= ob1; }
-            else { kb -= zb; lb = Z + ob0; hb = Z + ob1; rb |= 1 << l; }
+            const int o0 = rk(row, lo), o1 = rk(row, hi);
+            const int z = (hi - o1) - (lo - o0);
+            if (k < z) { lo -= o0; hi -= o1; }
+            else { k -= z; const int Z = s_Z[l]; lo = Z + o0; hi = Z + o1; r |= 1 << l; }
         }
+        return r;
     };
     int vfirst = INT_MAX, vlast = -1;
     for (int64_t i = tid; i < n; i += WM_T) {
@@ -322,7 +561,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
         const int64_t nobs = e > lo ? e - lo : 0;
         double res = __builtin_nan("");
         if (nobs >= minp && nobs > 0) {
-            const int plo = (int)(lo - t0), phi = (int)(e - t0);
+            const int plo = kidx((int)(lo - t0)), phi = kidx((int)(e - t0));
             double idxf = 0;
             int64_t k = 0;
             if (nobs > 1) {
@@ -330,13 +569,20 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
                 k = (int64_t)idxf;
             }
             const bool interp = !(nobs == 1 || (double)k == idxf);
-            int ra, rb;
-            kth2(plo, phi, (int)k, ra, rb);   /* rb is meaningless when !interp (k+1 may equal nobs) */
-            const double va = sv[ra];
+            const int ra = kth(plo, phi, (int)k);
+            const double va = svl ? svl[ra] : dval(t0 + spos(posR[ra]));
             if (!interp) {
                 res = va;
             } else {
-                const double vb = sv[rb];
+                /* k + 1 < (kept samples in the window) here, so an in-window
+                 * rank above ra exists: the successor in the window */
+                int rb = ra + 1, pb;
+                for (;;) {
+                    pb = posR[rb];
+                    if (pb >= plo && pb < phi) break;
+                    ++rb;
+                }
+                const double vb = svl ? svl[rb] : dval(t0 + spos(pb));
                 res = va + (vb - va) * (idxf - (double)k);
             }
             vfirst = vfirst < (int)i ? vfirst : (int)i;
@@ -367,5 +613,8 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm(RollqArgs A, double *sorted_s
     for (int64_t i = tid; i < first; i += WM_T) out[i] = vf;
     for (int64_t i = last + 1 + tid; i < n; i += WM_T) out[i] = vl;
 }
+
+template __global__ void k_rollq_wm_t<true>(RollqArgs, uint16_t *, int32_t *);
+template __global__ void k_rollq_wm_t<false>(RollqArgs, uint16_t *, int32_t *);
 
 }  // namespace bpmx

@@ -71,13 +71,15 @@ enum bpmx_file_flag {
 
 enum bpmx_option {
     BPMX_OPT_ROLLQ_MERGE = 1, /* force the sorted-union rolling quantile (test/diagnostic; default picks the
-                                 wavelet-matrix kernel for recordings of <= 20480 decimated samples) */
+                                 wavelet-matrix kernel for recordings of <= 18432 decimated samples) */
     BPMX_OPT_NATIVE_F64 = 2,  /* native mode: f64 VALU block projections instead of the exact-integer
                                  matrix-core kernel (test/diagnostic) */
     BPMX_OPT_HILBERT_ROCFFT = 4, /* native mode: rocFFT R2C/C2R Hilbert instead of the fused in-LDS transform
                                     (test/diagnostic; recordings the fused kernel cannot plan always use it) */
-    BPMX_OPT_DRAFT_FULL = 8      /* compute the draft floor (first rolling quantile) in full for every recording
+    BPMX_OPT_DRAFT_FULL = 8,     /* compute the draft floor (first rolling quantile) in full for every recording
                                     instead of deciding troughs from its bounds first (test/diagnostic) */
+    BPMX_OPT_ROLLQ_NOPRUNE = 16  /* wavelet-matrix rolling quantile over every sample, without first dropping
+                                    the samples no window's quantile can reach (test/diagnostic) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

@@ -48,7 +48,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&d_cand, env.size() * 4));
     CK(hipMalloc(&d_nout, F * 4));
     CK(hipMalloc(&d_state, env.size()));
-    CK(hipMalloc(&d_st, (size_t)F * 64));
+    CK(hipMalloc(&d_st, (size_t)F * 16 * 8));
     CK(hipMemcpy(d_env, env.data(), env.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_qv, qv.data(), qv.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_doff, doff.data(), (F + 1) * 8, hipMemcpyHostToDevice));
@@ -76,13 +76,13 @@ int main(int argc, char **argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             best = std::min(best, ms);
         }
-        std::vector<unsigned long long> st((size_t)F * 8);
+        std::vector<unsigned long long> st((size_t)F * 16);
         CK(hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost));
         std::vector<int32_t> no(F);
         CK(hipMemcpy(no.data(), d_nout, F * 4, hipMemcpyDeviceToHost));
         double sum[8] = {0}, tot = 0;
         for (int64_t f = 0; f < F; ++f)
-            for (int k = 0; k < 8; ++k) sum[k] += (double)st[f * 8 + k];
+            for (int k = 0; k < 8; ++k) sum[k] += (double)st[f * 16 + k];
         for (int k = 0; k < 8; ++k) tot += sum[k];
         long long np = 0;
         for (auto v : no) np += v;

@@ -31,7 +31,7 @@ int main(int argc, char **argv) {
     std::vector<int32_t> act(F, 1);
     double *dy, *denv; int64_t *dd; int32_t *da; double2 *dt; unsigned long long *dst;
     CK(hipMalloc(&dy, y.size() * 8)); CK(hipMalloc(&denv, y.size() * 8)); CK(hipMalloc(&dd, (F + 1) * 8));
-    CK(hipMalloc(&da, F * 4)); CK(hipMalloc(&dt, tabs.size() * 16)); CK(hipMalloc(&dst, (size_t)F * 64));
+    CK(hipMalloc(&da, F * 4)); CK(hipMalloc(&dt, tabs.size() * 16)); CK(hipMalloc(&dst, (size_t)F * 16 * 8));
     CK(hipMemcpy(dy, y.data(), y.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dd, doff.data(), (F + 1) * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(da, act.data(), F * 4, hipMemcpyHostToDevice));
@@ -49,10 +49,10 @@ int main(int argc, char **argv) {
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    std::vector<unsigned long long> st((size_t)F * 8);
+    std::vector<unsigned long long> st((size_t)F * 16);
     CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
     double acc[8] = {0};
-    for (int f = 0; f < F; ++f) for (int k = 0; k < 8; ++k) acc[k] += (double)st[(size_t)f * 8 + k];
+    for (int f = 0; f < F; ++f) for (int k = 0; k < 8; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
     printf("kernel %.4f ms;  mean cycles per workgroup (s_memtime):", ms / R);
     const char *nm[8] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "rollmean"};
     double tot = 0;
