@@ -204,6 +204,43 @@ def test_rolling_quantile_kernels_agree(det, name):
         _check_file(r, g)
 
 
+def _floor_envelopes():
+    """Envelopes that stress the final-floor pruning: golden env cases, the
+    vulpine labeler envelope, near-constant floors (ulp-level differences),
+    steep trends, random roughness, > WM_TRMAX troughs (unpruned path) and
+    short recordings dominated by edge windows."""
+    rng = np.random.default_rng(7)
+    out = [(G.load(n)["env"], int(G.load(n)["sr"])) for n in G.names(kind="env")]
+    g = G.load("vulpine")
+    out.append((O.rolling_mean(np.abs(g["pcm"]).astype(np.float64), int(g["fs"]) // 10, 1), 302))
+    n = 18124
+    t = np.arange(n)
+    beat = np.maximum(0.0, np.sin(2 * np.pi * t / 250.0)) ** 8
+    out.append((10.0 + np.spacing(10.0) * rng.integers(0, 5, n) + 300 * beat, 302))         # ulp-level floor
+    out.append((10.0 + 0.05 * t + 3000 * beat + rng.random(n), 302))                           # ramp
+    out.append((rng.random(n) ** 3 * 1000 + 50 * beat, 302))                                   # rough
+    out.append((np.abs(np.sin(t / 9.0)) * 100 + rng.random(n), 302))                           # > 512 troughs
+    out.append((200 + 80 * np.sin(t / 700.0) + 300 * beat + rng.random(n), 302))              # slow wander
+    out.append((300 * beat[:4000] + rng.random(4000) + 20, 302))                               # short
+    return out
+
+
+def test_rollq_pruning_exact(det):
+    """The pruned wavelet-matrix floor (default) equals the unpruned one
+    (BPMX_OPT_ROLLQ_NOPRUNE) and the oracle bit for bit on every envelope."""
+    from bpm_analysis_amd import _native as N
+    params = dict(G.BASE_PARAMS)
+    for env, sr in _floor_envelopes():
+        a = det.run_env_host([env], sr, params, N.STAGE_FLOOR)[0]
+        b = det.run_env_host([env], sr, params, N.STAGE_FLOOR, options=N.OPT_ROLLQ_NOPRUNE)[0]
+        assert _same(a["floor"], b["floor"])
+        assert _same(a["troughs"], b["troughs"])
+        d = O.derive(sr, params)
+        of, ot, _ = O.noise_floor(env, d, params)
+        assert _same(a["floor"], of)
+        assert _same(a["troughs"], ot)
+
+
 @pytest.mark.parametrize("fs", [44100, 22050, 48000])
 def test_native_block_kernels_agree(det, fs):
     """The exact-integer matrix-core block projections (default for int16 mono,
