@@ -40,6 +40,18 @@ int fail(int code, const std::string &msg) {
 
 namespace {
 
+/* per-run output init from the cached device geometry (no pageable H2D copy
+ * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
+__global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *active, int32_t *flags, int32_t *ntr,
+                                                  int32_t *npk, int32_t *runs) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= n_files) return;
+    flags[f] = active[f] ? 0 : BPMX_F_TOO_SHORT;
+    if (ntr) ntr[f] = 0;
+    if (npk) npk[f] = 0;
+    for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
+}
+
 __global__ __launch_bounds__(64) void k_synth_beats(uint64_t seed0, int n_files, const int64_t *foff,
                                                     const int64_t *boff, int32_t fs, int64_t *s1, int64_t *s2,
                                                     int32_t *nb) {
@@ -155,7 +167,17 @@ int bpmx_synth(bpmx_ctx *ctx, uint64_t seed0, int32_t n_files, const int64_t *fr
 int bpmx_profile(bpmx_ctx *ctx, int on) {
     if (!ctx) return fail(BPMX_E_ARG, "ctx is NULL");
     ctx->prof = on != 0;
-    if (on) ctx->totals.clear();
+    if (on) {
+        ctx->totals.clear();
+        /* events created now, not inside the profiled launches (hipEventCreate
+         * on the launch path leaves the GPU waiting on the host) */
+        HIP_TRY(hipSetDevice(ctx->device));
+        while (ctx->pool.size() < 4096) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            ctx->pool.push_back(e);
+        }
+    }
     return BPMX_OK;
 }
 
@@ -210,7 +232,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
 
     /* ---- geometry ---- */
     std::vector<int64_t> foff(F + 1), doff(F + 1), boff(F + 1);
-    std::vector<int32_t> active(F), flags0(F);
+    std::vector<int32_t> active(F);
     int64_t maxnd = 0;
     foff[0] = 0; doff[0] = 0; boff[0] = 0;
     for (int f = 0; f < F; ++f) {
@@ -223,7 +245,6 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         maxnd = std::max(maxnd, nd);
         const bool ok = do_env ? nd > 15 : nd >= 1;
         active[f] = ok ? 1 : 0;
-        flags0[f] = ok ? 0 : BPMX_F_TOO_SHORT;
         if (nd >= (int64_t)INT_MAX / 2) return fail(BPMX_E_LIMIT, "recording too long");
     }
     const int64_t sumnd = doff[F], sumb = boff[F];
@@ -253,10 +274,8 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     const int32_t *d_active = di;
     int32_t *d_run1 = di + F, *d_run2 = di + 2 * F, *d_an1 = di + 3 * F, *d_an2 = di + 4 * F, *d_nraw = di + 5 * F;
 
-    HIP_TRY(hipMemcpyAsync(O->flags, flags0.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
-    if (do_floor) HIP_TRY(hipMemsetAsync(O->n_troughs, 0, (size_t)F * 4, s));
-    if (do_peaks) HIP_TRY(hipMemsetAsync(O->n_peaks, 0, (size_t)F * 4, s));
-    HIP_TRY(hipMemsetAsync(d_run1, 0, (size_t)F * 4 * 5, s));
+    LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, F, d_active, (int32_t *)O->flags,
+           do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1);
 
     /* ---- ENVELOPE ---- */
     if (do_env) {

@@ -365,10 +365,19 @@ __device__ __forceinline__ void st_state(uint8_t *p, uint8_t v) {
 }
 
 constexpr int FP_T = 1024;
+#ifndef BPMX_FP_NP
+#define BPMX_FP_NP 2      /* prominences per wave per round (their loads overlap) */
+#endif
+#ifndef BPMX_FP_G
+#define BPMX_FP_G 8       /* local-maxima iterations per load group */
+#endif
+#ifndef BPMX_FP_LB
+#define BPMX_FP_LB 8      /* min waves per EU (register budget) */
+#endif
 constexpr int FP_NBMAX = 2048;   /* block tables staged in LDS up to 131072 samples */
 constexpr int FP_MC = 2048;      /* candidates kept in LDS up to this many */
 
-__global__ __launch_bounds__(FP_T, 8) void k_find_peaks(PeakArgs A) {
+__global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f]) return;
     const int64_t d0 = A.doff[f];
@@ -398,7 +407,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks(PeakArgs A) {
     /* (1)+(2) local maxima with plateau midpoints, height filter.  Position
      * i = 1 + (g*FP_G + it)*FP_T + tid; a group of FP_G iterations issues its
      * loads together, then one (iteration, wave)-ordered scan places the hits. */
-    constexpr int FP_G = 8;
+    constexpr int FP_G = BPMX_FP_G;
     __shared__ int s_gc[FP_G][FP_T / 64];
     int m = 0;
     const int64_t iters = n > 2 ? (n - 2 + FP_T - 1) / FP_T : 0;
@@ -524,7 +533,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks(PeakArgs A) {
     const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
     /* the kept candidates are taken NP at a time per wave so that their global
      * loads overlap */
-    constexpr int NP = 2;
+    constexpr int NP = BPMX_FP_NP;
     {
         const int nw = FP_T / 64, wv = wave_id();
         int j = wv;
