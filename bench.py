@@ -60,6 +60,8 @@ def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, 
         # final floor: dense (interpolated in-kernel from the troughs) in, floor out; the
         # draft pass runs only for recordings with an undecided trough (none on this workload)
         "k_rollq_wm": F * nd * 8,
+        "k_rollq_wm[full]": 0,                              # unpruned variant: recordings the pruned one flags (none here)
+        "k_init_out": 0,
         "k_rolling_quantile": F * nd * 16,
         "k_floor_final": 0, "k_sanitize": 0, "k_interp": 0,
     }
@@ -76,6 +78,7 @@ def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, 
 
 # launch labels -> kernel names in the rocprofv3 PMC summary
 PMC_NAMES = {"k_native_blocks": ("k_native_blocks_mfma", "k_native_blocks_i16", "k_native_blocks_gen"),
+             "k_rollq_wm": ("k_rollq_wm_t",),
              "k_find_peaks[troughs]": ("k_find_peaks",), "k_find_peaks[peaks]": ("k_find_peaks",)}
 
 

@@ -22,7 +22,8 @@ import re
 
 def short_name(kernel: str) -> str:
     k = kernel.split("(")[0]
-    k = re.sub(r"<.*", "", k).replace("void ", "").strip()
+    full = "k_rollq_wm_t<false>" in k                 # the unpruned rolling-quantile variant
+    k = re.sub(r"<.*", "", k).replace("void ", "").strip() + ("[full]" if full else "")
     k = k.split("::")[-1]
     if "fft" in kernel.lower() or "bluestein" in kernel.lower():
         return "rocfft:" + k
