@@ -178,6 +178,44 @@ def test_native_tile_geometries(det, fs, lens, shift):
         _check_file(h, o, exact_env=False)
 
 
+@pytest.mark.parametrize("mode", ["native", "reference"])
+def test_config_c2_ten_minute_recording(det, mode):
+    """BASELINE config C2: one 10-min 44.1 kHz mono recording (Nd = 181,233:
+    the long-recording kernels — sorted-union rolling quantile, global block
+    tables, multi-pass quantile) against the oracle."""
+    fs, n = 44100, 44100 * 600
+    pcm = O.synth(4242, n, fs, 1)
+    params = dict(G.BASE_PARAMS)
+    r = det.run_host([pcm], fs, params, mode=mode, want_y=True)[0]
+    o = O.detect(pcm, fs, params, mode=mode)
+    if mode == "native":
+        scale = np.max(np.abs(o["y"]))
+        assert np.max(np.abs(r["y"] - o["y"])) <= 1e-9 * scale
+    _check_file(r, o, exact_env=(mode == "reference"))
+    assert len(r["peaks"]) > 1000
+
+
+def test_config_c5_96k_stereo_ragged(det):
+    """BASELINE config C5 (scaled down in length): 96 kHz stereo recordings of
+    ragged lengths in one batch (ds = 300, two channels averaged on device),
+    native mode, against the oracle."""
+    import torch
+    fs = 96000
+    lens = [96000 * 150 + 17, 96000 * 61, 96000 * 247 + 3]
+    recs = [O.synth(700 + i, n, fs, 2) for i, n in enumerate(lens)]
+    dev = torch.from_numpy(np.concatenate([r.reshape(-1) for r in recs])).to(det.device)
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    res = det.run(dev, fo, fs, params, mode="native", channels=2, want_y=True)
+    torch.cuda.synchronize()
+    for h, pcm in zip(res.to_host(), recs):
+        o = O.detect(pcm, fs, params, mode="native")
+        assert h["sr"] == o["sr"] == 320
+        scale = np.max(np.abs(o["y"]))
+        assert np.max(np.abs(h["y"] - o["y"])) <= 1e-9 * scale
+        _check_file(h, o, exact_env=False)
+
+
 def test_reference_side_ctypes_stub():
     """INTEGRATION.md's torch-free ctypes binding of the C ABI, on a golden."""
     import importlib.util
