@@ -33,6 +33,8 @@
 #include <tuple>
 #include <vector>
 
+#include <complex>
+
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 #include "bpmx_native.h"
@@ -40,11 +42,16 @@
 
 namespace bpmx {
 
-/* table layout (native_tables.pack) */
-enum { TB_A = 0, TB_B = 16, TB_C = 20, TB_D = 24, TB_M = 25, TB_P = 41, TB_ZI = 57, TB_COEF = 64 };
+/* table layout (native_tables.pack).  Every block/tile table is in MODAL
+ * coordinates S' = V^-1 S, in which the cascade's state matrix is two 2x2
+ * rotation-scaling blocks (its two conjugate pole pairs); TB_V holds V (the
+ * original-coordinate slot TB_A is not needed on the device). */
+enum { TB_A = 0, TB_V = 0, TB_B = 16, TB_C = 20, TB_D = 24, TB_M = 25, TB_P = 41, TB_ZI = 57, TB_COEF = 64 };
 
-/* tile tables, after the coefficient rows (native_tables.tile_tables) */
-enum { TT_KPOW = 0, TT_MT = 96, TT_G0 = 112, TT_ALPHA = 128, TT_BETA = 384, TT_SIZE = 640 };
+/* tile tables, after the coefficient rows (native_tables.tile_tables):
+ * TT_KPOW holds M'^(2^k), k = 0..5, as (a1, b1, a2, b2) per power — the
+ * blocks [[a, b], [-b, a]] — in its first 24 doubles; TT_VI = V^-1 */
+enum { TT_KPOW = 0, TT_MT = 96, TT_G0 = 112, TT_ALPHA = 128, TT_BETA = 384, TT_VI = 640, TT_SIZE = 656 };
 constexpr int NAT_PART = 16;          /* doubles per partial-tile block record: u4 v4 x pad3 S4 */
 
 struct NatTile {
@@ -119,6 +126,12 @@ __device__ __forceinline__ V4 mv(const M4 &M, const V4 &x) {
     r.c = __builtin_fma(M.m[8], x.a, __builtin_fma(M.m[9], x.b, __builtin_fma(M.m[10], x.c, M.m[11] * x.d)));
     r.d = __builtin_fma(M.m[12], x.a, __builtin_fma(M.m[13], x.b, __builtin_fma(M.m[14], x.c, M.m[15] * x.d)));
     return r;
+}
+/* block-diagonal rotation form: r = (a1, b1, a2, b2), M = diag([[a1, b1], [-b1, a1]], [[a2, b2], [-b2, a2]]) */
+__device__ __forceinline__ V4 mv_rot(const double *r, const V4 &x) {
+    const double a1 = r[0], b1 = r[1], a2 = r[2], b2 = r[3];
+    return V4{__builtin_fma(a1, x.a, b1 * x.b), __builtin_fma(a1, x.b, -b1 * x.a), __builtin_fma(a2, x.c, b2 * x.d),
+              __builtin_fma(a2, x.d, -b2 * x.c)};
 }
 __device__ __forceinline__ V4 add4(const V4 &x, const V4 &y) { return V4{x.a + y.a, x.b + y.b, x.c + y.c, x.d + y.d}; }
 __device__ __forceinline__ M4 mm(const M4 &X, const M4 &Y) {
@@ -220,7 +233,7 @@ __device__ __forceinline__ double dot4(const V4 &a, const V4 &b) {
 /* The epilogue's constants, staged in LDS once per workgroup: a vector load
  * here would sit behind the next tile's prefetch in vmcnt order and stall the
  * wave until the whole prefetch landed. */
-enum { ET_KPOW = 0, ET_P = 96, ET_C = 112, ET_D = 116, ET_SIZE = 117 };
+enum { ET_KPOW = 0, ET_P = 24, ET_C = 40, ET_D = 44, ET_SIZE = 45 };
 __device__ __forceinline__ void nat_stage_epilogue_tables(const NatBlockArgs &A, double *et) {
     for (int i = threadIdx.x; i < ET_SIZE; i += blockDim.x) {
         double v;
@@ -246,13 +259,13 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const d
         return;
     }
     if (!valid) { u = V4{0, 0, 0, 0}; v = V4{0, 0, 0, 0}; x = 0; }
-    /* incl_b = sum_{c<=b} M^(b-c) u_c */
+    /* incl_b = sum_{c<=b} M^(b-c) u_c  (modal: M^d is two 2x2 rotation blocks) */
     V4 incl = u;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const int d = 1 << k;
         const V4 y = shfl_up_v(incl, d);
-        if (lane >= d) incl = add4(incl, mv(nat_ld16(et + ET_KPOW + 16 * k), y));
+        if (lane >= d) incl = add4(incl, mv_rot(et + ET_KPOW + 4 * k, y));
     }
     V4 loc = shfl_up_v(incl, 1);
     if (lane == 0) loc = V4{0, 0, 0, 0};
@@ -262,7 +275,7 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const d
     for (int k = 0; k < 6; ++k) {
         const int d = 1 << k;
         const V4 y = shfl_down_v(R, d);
-        if (lane + d < 64) R = add4(R, mv(nat_ld16(et + ET_KPOW + 16 * k), y));
+        if (lane + d < 64) R = add4(R, mv_rot(et + ET_KPOW + 4 * k, y));
     }
     const V4 C = nat_ld4(et + ET_C);
     const double D = et[ET_D];
@@ -626,6 +639,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     const V4 Cv = nat_ld4(tb + TB_C);
     const double Dd = tb[TB_D];
     const V4 zi = nat_ld4(tb + TB_ZI);
+    const M4 Vm = nat_ld16(tb + TB_V), Vi = nat_ld16(tt + TT_VI);   /* modal <-> original state */
     const double *agg = A.agg + t0 * 8;
     double *car = A.carry + t0 * 8;
     double *yd = A.yd + A.doff[f];
@@ -638,7 +652,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         const double e0 = odd_ext(wdt, x0, s_head[15]);
         V4 z{zi.a * e0, zi.b * e0, zi.c * e0, zi.d * e0};
         for (int k = 0; k < 15; ++k) (void)SS.step(z, odd_ext(wdt, x0, s_head[15 - k]));
-        S = z;
+        S = mv(Vi, z);                                      /* tables are modal */
     }
     /* forward tile carries: car[t][0..3] = S0_t */
     for (int64_t c0 = 0; c0 < Tf; c0 += NC_CH) {
@@ -668,7 +682,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         const int64_t nt = ntl + 15;                            /* tail length incl. right pad */
         const double xl = xt(n - 1);
         {
-            V4 z = S;
+            V4 z = mv(Vm, S);                               /* the exact recursion runs in the original basis */
             for (int64_t k = 0; k < nt; ++k) {
                 const int64_t xi = base + k;
                 const double u = xi < n ? xt(xi) : odd_ext(wdt, xl, xt(n - 2 - (xi - n)));
@@ -678,6 +692,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         const double y0 = s_ytl[nt - 1];
         q = V4{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
         for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, s_ytl[k]);
+        q = mv(Vi, q);
         yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
         for (int b = Lp - 1; b >= 0; --b) {
             const double *r = pp + b * NAT_PART;
@@ -844,6 +859,77 @@ void lm_vec(const LM &X, const LD *v, LD *out) {
     }
 }
 
+/* real basis of the two conjugate eigenvector pairs of A: V, V^-1.  False
+ * when A has a real eigenvalue (then M' would not be two rotation blocks). */
+bool modal_basis(const LM &A, LM *V, LM *Vi) {
+    typedef std::complex<LD> CX;
+    /* eigenvalues: A is block lower-triangular, its diagonal blocks are the
+     * sections' companion forms [[-a1, 1], [-a2, 0]] */
+    CX lam[2];
+    for (int b = 0; b < 2; ++b) {
+        const LD a1 = -A.m[(2 * b) * 4 + 2 * b], a2 = -A.m[(2 * b + 1) * 4 + 2 * b];
+        const LD disc = a1 * a1 - 4 * a2;
+        if (disc >= 0) return false;
+        lam[b] = CX(-a1 / 2, sqrtl(-disc) / 2);
+    }
+    for (int b = 0; b < 2; ++b) {
+        /* null vector of (A - lam I) by Gaussian elimination with partial pivoting */
+        CX M[4][4];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) M[i][j] = CX(A.m[i * 4 + j], 0) - (i == j ? lam[b] : CX(0, 0));
+        int piv_col[4], rank = 0;
+        bool is_piv[4] = {false, false, false, false};
+        for (int c = 0; c < 4 && rank < 4; ++c) {
+            int best = -1;
+            LD bv = 0;
+            for (int r = rank; r < 4; ++r)
+                if (std::abs(M[r][c]) > bv) { bv = std::abs(M[r][c]); best = r; }
+            if (best < 0 || bv < 1e-14L) continue;
+            for (int j = 0; j < 4; ++j) std::swap(M[rank][j], M[best][j]);
+            for (int r = 0; r < 4; ++r) {
+                if (r == rank) continue;
+                const CX fct = M[r][c] / M[rank][c];
+                for (int j = 0; j < 4; ++j) M[r][j] -= fct * M[rank][j];
+            }
+            piv_col[rank++] = c;
+            is_piv[c] = true;
+        }
+        if (rank != 3) return false;
+        int fr = 0;
+        while (is_piv[fr]) ++fr;
+        CX v[4];
+        v[fr] = CX(1, 0);
+        for (int r = 0; r < rank; ++r) v[piv_col[r]] = -M[r][fr] / M[r][piv_col[r]];
+        /* A (vr + i vi) = lam (vr + i vi): in the basis [vr, vi] the block is
+         * [[Re, Im], [-Im, Re]] (column convention, see build_tables) */
+        for (int i = 0; i < 4; ++i) {
+            V->m[i * 4 + 2 * b] = v[i].real();
+            V->m[i * 4 + 2 * b + 1] = v[i].imag();
+        }
+    }
+    /* V^-1 by Gauss-Jordan */
+    LD W[4][8];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) W[i][j] = j < 4 ? V->m[i * 4 + j] : (j - 4 == i ? 1 : 0);
+    for (int c = 0; c < 4; ++c) {
+        int best = c;
+        for (int r = c + 1; r < 4; ++r)
+            if (fabsl(W[r][c]) > fabsl(W[best][c])) best = r;
+        if (fabsl(W[best][c]) < 1e-30L) return false;
+        for (int j = 0; j < 8; ++j) std::swap(W[c][j], W[best][j]);
+        const LD d = W[c][c];
+        for (int j = 0; j < 8; ++j) W[c][j] /= d;
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            const LD fct = W[r][c];
+            for (int j = 0; j < 8; ++j) W[r][j] -= fct * W[c][j];
+        }
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) Vi->m[i * 4 + j] = W[i][4 + j];
+    return true;
+}
+
 std::vector<double> build_tables(const double *sos, const double *sos_zi, int L, int T, std::vector<LD> *coefld) {
     /* probe the cascade step: s' = A s + B u, y = C s + D u */
     auto step = [&](const LD *z, LD u, LD *zo) -> LD {
@@ -868,6 +954,35 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L,
         LD e[4] = {0, 0, 0, 0};
         D = step(e, 1, Bv);
     }
+    /* modal coordinates: V = [Re v1, Im v1, Re v2, Im v2] from one eigenvector
+     * of each conjugate pole pair, so V^-1 A V = diag(R(l1), R(l2)) with
+     * R(l) = [[Re l, Im l], [-Im l, Re l]].  The blocks are then set to that
+     * exact form (the off-block residue of the long-double transform is
+     * ~1e-19 relative and is dropped), B' = V^-1 B, C' = C V. */
+    LM V{}, Vi{};
+    const bool modal = modal_basis(A, &V, &Vi);
+    if (modal) {
+        const LM Am = lm_mul(Vi, lm_mul(A, V));
+        LM R{};
+        for (int b = 0; b < 2; ++b) {
+            const int o = 2 * b;
+            const LD re = (Am.m[o * 4 + o] + Am.m[(o + 1) * 4 + o + 1]) / 2;
+            const LD im = (Am.m[o * 4 + o + 1] - Am.m[(o + 1) * 4 + o]) / 2;
+            R.m[o * 4 + o] = re; R.m[o * 4 + o + 1] = im;
+            R.m[(o + 1) * 4 + o] = -im; R.m[(o + 1) * 4 + o + 1] = re;
+        }
+        A = R;
+        LD b2[4], c2[4];
+        lm_vec(Vi, Bv, b2);
+        for (int c = 0; c < 4; ++c) {
+            LD acc = 0;
+            for (int k = 0; k < 4; ++k) acc += Cv[k] * V.m[k * 4 + c];
+            c2[c] = acc;
+        }
+        for (int k = 0; k < 4; ++k) { Bv[k] = b2[k]; Cv[k] = c2[k]; }
+    } else {                                  /* real poles: stay in the original basis */
+        for (int i = 0; i < 16; ++i) V.m[i] = Vi.m[i] = (i % 5 == 0) ? 1 : 0;
+    }
     std::vector<LM> pw(L + 2);
     for (int i = 0; i < 16; ++i) pw[0].m[i] = (i % 5 == 0) ? 1 : 0;
     for (int i = 1; i <= L + 1; ++i) pw[i] = lm_mul(A, pw[i - 1]);
@@ -891,7 +1006,7 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L,
             for (int c = 0; c < 4; ++c) P.m[r * 4 + c] += AB[(size_t)(i - 1) * 4 + r] * CA[c];
     }
     std::vector<double> out(64 + 8 * (size_t)(L + 1) + TT_SIZE, 0.0);
-    for (int i = 0; i < 16; ++i) out[TB_A + i] = (double)A.m[i];
+    for (int i = 0; i < 16; ++i) out[TB_V + i] = (double)V.m[i];
     for (int i = 0; i < 4; ++i) { out[TB_B + i] = (double)Bv[i]; out[TB_C + i] = (double)Cv[i]; }
     out[TB_D] = (double)D;
     for (int i = 0; i < 16; ++i) { out[TB_M + i] = (double)pw[L].m[i]; out[TB_P + i] = (double)P.m[i]; }
@@ -937,10 +1052,14 @@ std::vector<double> build_tables(const double *sos, const double *sos_zi, int L,
         };
         double *tt = &out[TB_COEF + 8 * (size_t)(L + 1)];
         LM K = M;
-        for (int k = 0; k < 6; ++k) {
-            for (int i = 0; i < 16; ++i) tt[TT_KPOW + 16 * k + i] = (double)K.m[i];
+        for (int k = 0; k < 6; ++k) {             /* rotation form (a1, b1, a2, b2); M' is block diagonal */
+            tt[TT_KPOW + 4 * k + 0] = (double)K.m[0];
+            tt[TT_KPOW + 4 * k + 1] = (double)K.m[1];
+            tt[TT_KPOW + 4 * k + 2] = (double)K.m[10];
+            tt[TT_KPOW + 4 * k + 3] = (double)K.m[11];
             K = lm_mul(K, K);
         }
+        for (int i = 0; i < 16; ++i) tt[TT_VI + i] = (double)Vi.m[i];
         for (int i = 0; i < 16; ++i) { tt[TT_MT + i] = (double)Mp[T].m[i]; tt[TT_G0 + i] = (double)G[0].m[i]; }
         for (int b = 0; b < T; ++b) {
             LD al[4], cg[4], cm[4];
