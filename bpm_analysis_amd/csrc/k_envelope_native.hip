@@ -39,6 +39,7 @@
 #include "bpmx_kernels.h"
 #include "bpmx_native.h"
 #include "bpmx_hilbert.h"
+#include "bpmx_xlane.h"
 
 namespace bpmx {
 
@@ -172,6 +173,15 @@ __device__ __forceinline__ V4 shfl_up_v(const V4 &x, int d) {
 __device__ __forceinline__ V4 shfl_down_v(const V4 &x, int d) {
     return V4{__shfl_down(x.a, d), __shfl_down(x.b, d), __shfl_down(x.c, d), __shfl_down(x.d, d)};
 }
+/* register-only V4 shifts (bpmx_xlane.h), for the tile epilogue's scans */
+template <int D>
+__device__ __forceinline__ V4 xl_up_v(const V4 &x) {
+    return V4{xl_up<D>(x.a), xl_up<D>(x.b), xl_up<D>(x.c), xl_up<D>(x.d)};
+}
+template <int D>
+__device__ __forceinline__ V4 xl_down_v(const V4 &x) {
+    return V4{xl_down<D>(x.a), xl_down<D>(x.b), xl_down<D>(x.c), xl_down<D>(x.d)};
+}
 __device__ __forceinline__ M4 mpow(const M4 &X, int64_t e) {
     M4 R = eye4(), P = X;
     while (e > 0) {
@@ -261,22 +271,27 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const d
     if (!valid) { u = V4{0, 0, 0, 0}; v = V4{0, 0, 0, 0}; x = 0; }
     /* incl_b = sum_{c<=b} M^(b-c) u_c  (modal: M^d is two 2x2 rotation blocks) */
     V4 incl = u;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const int d = 1 << k;
-        const V4 y = shfl_up_v(incl, d);
-        if (lane >= d) incl = add4(incl, mv_rot(et + ET_KPOW + 4 * k, y));
+    /* Kogge-Stone steps; the one-lane shifts are DPP (wave_shr/shl:1), the
+     * longer ones ds_bpermute (measured: the DPP + permlane composites of
+     * bpmx_xlane.h cost more VALU than they save in LDS latency here) */
+#define NAT_UP(K)                                                            \
+    {                                                                        \
+        const V4 y = K == 0 ? xl_up_v<1>(incl) : shfl_up_v(incl, 1 << K);   \
+        if (lane >= (1 << K)) incl = add4(incl, mv_rot(et + ET_KPOW + 4 * K, y)); \
     }
-    V4 loc = shfl_up_v(incl, 1);
+    NAT_UP(0) NAT_UP(1) NAT_UP(2) NAT_UP(3) NAT_UP(4) NAT_UP(5)
+#undef NAT_UP
+    V4 loc = xl_up_v<1>(incl);
     if (lane == 0) loc = V4{0, 0, 0, 0};
     /* R_b = sum_{c>=b} M^(c-b) (P loc_c + v_c) */
     V4 R = valid ? add4(mv(nat_ld16(et + ET_P), loc), v) : V4{0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const int d = 1 << k;
-        const V4 y = shfl_down_v(R, d);
-        if (lane + d < 64) R = add4(R, mv_rot(et + ET_KPOW + 4 * k, y));
+#define NAT_DOWN(K)                                                          \
+    {                                                                        \
+        const V4 y = K == 0 ? xl_down_v<1>(R) : shfl_down_v(R, 1 << K);      \
+        if (lane + (1 << K) < 64) R = add4(R, mv_rot(et + ET_KPOW + 4 * K, y)); \
     }
+    NAT_DOWN(0) NAT_DOWN(1) NAT_DOWN(2) NAT_DOWN(3) NAT_DOWN(4) NAT_DOWN(5)
+#undef NAT_DOWN
     const V4 C = nat_ld4(et + ET_C);
     const double D = et[ET_D];
     if (valid) A.gam[tl.gbase + lane] = dot4(C, R) + D * dot4(C, loc) + D * D * x;
