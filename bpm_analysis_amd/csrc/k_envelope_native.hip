@@ -615,15 +615,37 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
 template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 template __global__ void k_native_blocks_mfma<5>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 
-/* One wave per recording (lane 0 carries the sequential recursions):
- *   head  15 padded samples, exact sosfilt steps -> S at block 0;
- *   tiles S0_(t+1) = M^T S0_t + incl_t (forward carries, stored per tile);
+/* One wave per recording:
+ *   head  15 padded samples, exact sosfilt steps -> S at block 0 (lane 0);
+ *   tiles S0_(t+1) = M^T S0_t + incl_t (forward carries, stored per tile):
+ *         a parallel affine scan — lane l composes its run of tiles into one
+ *         map (P, a) (P a power of M^T: in modal coordinates two 2x2 rotation
+ *         blocks = two complex numbers), Kogge-Stone over the lanes, then each
+ *         lane replays its run from its carry-in;
  *   partial last tile: exact block recursion forward, then backward with
- *         its decimated outputs;
+ *         its decimated outputs (lane 0);
  *   tail  [c_(nd-1), ne): exact forward then backward per-sample recursion
- *         -> Q at block nb and yd[nd-1];
- *   tiles Qe_t stored, Q_start = M^T Qe_t + R0_t + G0 S0_t (backward). */
-constexpr int NC_CH = 64;             /* tiles per LDS chunk of the carry walks (small: many waves per CU) */
+ *         -> Q at block nb and yd[nd-1] (lane 0);
+ *   tiles Qe_t stored, Q_start = M^T Qe_t + R0_t + G0 S0_t (backward): the
+ *         same scan mirrored (maps composed right to left, shuffles down). */
+struct Cx2 { double a1, b1, a2, b2; };   /* diag([[a1, b1], [-b1, a1]], [[a2, b2], [-b2, a2]]) */
+__device__ __forceinline__ Cx2 cx2_mul(const Cx2 &x, const Cx2 &y) {
+    return Cx2{x.a1 * y.a1 - x.b1 * y.b1, x.a1 * y.b1 + x.b1 * y.a1, x.a2 * y.a2 - x.b2 * y.b2,
+               x.a2 * y.b2 + x.b2 * y.a2};
+}
+__device__ __forceinline__ V4 cx2_mv(const Cx2 &r, const V4 &x) {
+    return V4{r.a1 * x.a + r.b1 * x.b, -r.b1 * x.a + r.a1 * x.b, r.a2 * x.c + r.b2 * x.d, -r.b2 * x.c + r.a2 * x.d};
+}
+__device__ __forceinline__ Cx2 shfl_cx2(const Cx2 &x, int src) {
+    return Cx2{__shfl(x.a1, src), __shfl(x.b1, src), __shfl(x.a2, src), __shfl(x.b2, src)};
+}
+__device__ __forceinline__ Cx2 shfl_up_cx2(const Cx2 &x, int d) {
+    return Cx2{__shfl_up(x.a1, d), __shfl_up(x.b1, d), __shfl_up(x.a2, d), __shfl_up(x.b2, d)};
+}
+__device__ __forceinline__ Cx2 shfl_down_cx2(const Cx2 &x, int d) {
+    return Cx2{__shfl_down(x.a1, d), __shfl_down(x.b1, d), __shfl_down(x.a2, d), __shfl_down(x.b2, d)};
+}
+
 __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f]) return;
@@ -633,11 +655,9 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     const int ds = A.ds, bt = A.bt;
     const int64_t t0 = A.toff[f];
     const int64_t Tf = nb / bt;                             /* full tiles */
-    /* Everything lane 0's sequential recursions read comes through LDS first
-     * (plain ds_read, no aliasing with the stores): tile sums / carries in
-     * chunks of NC_CH tiles, the head's 16 samples, the tail's <= ds+1 samples
-     * (+16 for the mirror), the partial tile's block records. */
-    __shared__ double s_in[NC_CH * 8], s_out[NC_CH * 8];
+    /* what lane 0's sequential recursions read comes through LDS first: the
+     * head's 16 samples, the tail's <= ds+1 samples (+16 for the mirror), the
+     * partial tile's block records */
     __shared__ double s_head[16], s_tail[320 + 20], s_ytl[320 + 20], s_part[64 * NAT_PART];
     const int64_t n = A.foff[f + 1] - A.foff[f];
     const int64_t fb = A.foff[f];
@@ -650,7 +670,8 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     for (int k = lane; k < Lp * NAT_PART; k += 64) s_part[k] = A.part[(int64_t)f * 64 * NAT_PART + k];
     const int wdt = work_dtype(A.dtype, A.channels);
     const double *tb = A.tab, *tt = A.tt;
-    const M4 Mm = nat_ld16(tb + TB_M), Pm = nat_ld16(tb + TB_P), MT = nat_ld16(tt + TT_MT), G0 = nat_ld16(tt + TT_G0);
+    const M4 Mm = nat_ld16(tb + TB_M), Pm = nat_ld16(tb + TB_P), G0 = nat_ld16(tt + TT_G0);
+    const Cx2 MT{tt[TT_MT + 0], tt[TT_MT + 1], tt[TT_MT + 10], tt[TT_MT + 11]};   /* M^T, modal: rotation blocks */
     const V4 Cv = nat_ld4(tb + TB_C);
     const double Dd = tb[TB_D];
     const V4 zi = nat_ld4(tb + TB_ZI);
@@ -658,6 +679,11 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     const double *agg = A.agg + t0 * 8;
     double *car = A.carry + t0 * 8;
     double *yd = A.yd + A.doff[f];
+    const Cx2 ID{1, 0, 1, 0};
+    const V4 Z4{0, 0, 0, 0};
+    /* this lane's run of tiles [tb0, te0) */
+    const int64_t CH = (Tf + 63) / 64;
+    const int64_t tb0 = min<int64_t>(Tf, (int64_t)lane * CH), te0 = min<int64_t>(Tf, tb0 + CH);
 
     /* head: 15 padded samples -> S at block 0 */
     V4 S{0, 0, 0, 0};
@@ -669,20 +695,45 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         for (int k = 0; k < 15; ++k) (void)SS.step(z, odd_ext(wdt, x0, s_head[15 - k]));
         S = mv(Vi, z);                                      /* tables are modal */
     }
-    /* forward tile carries: car[t][0..3] = S0_t */
-    for (int64_t c0 = 0; c0 < Tf; c0 += NC_CH) {
-        const int cn = (int)(Tf - c0 < NC_CH ? Tf - c0 : NC_CH);
-        for (int k = lane; k < cn * 8; k += 64) s_in[k] = agg[c0 * 8 + k];
-        __syncthreads();
-        if (lane == 0) {
-            for (int t = 0; t < cn; ++t) {
-                s_out[t * 4 + 0] = S.a; s_out[t * 4 + 1] = S.b; s_out[t * 4 + 2] = S.c; s_out[t * 4 + 3] = S.d;
-                S = add4(mv(MT, S), V4{s_in[t * 8], s_in[t * 8 + 1], s_in[t * 8 + 2], s_in[t * 8 + 3]});
+    S = V4{__shfl(S.a, 0), __shfl(S.b, 0), __shfl(S.c, 0), __shfl(S.d, 0)};
+
+    /* forward tile carries: car[t][0..3] = S0_t; car[t][4..7] temporarily
+     * holds b_t = R0_t + G0 S0_t for the backward scan (same lane, same run) */
+    {
+        Cx2 P = ID;
+        V4 acc = Z4;
+        for (int64_t t = tb0; t < te0; ++t) {
+            acc = add4(cx2_mv(MT, acc), nat_ld4(agg + t * 8));
+            P = cx2_mul(MT, P);
+        }
+        /* inclusive Kogge-Stone over lanes: x_l <- x_l o x_(l-d) */
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int d = 1 << k;
+            const Cx2 Pe = shfl_up_cx2(P, d);
+            const V4 ae = shfl_up_v(acc, d);
+            if (lane >= d) {
+                acc = add4(cx2_mv(P, ae), acc);
+                P = cx2_mul(P, Pe);
             }
         }
-        __syncthreads();
-        for (int k = lane; k < cn * 4; k += 64) car[(c0 + k / 4) * 8 + (k & 3)] = s_out[k];
-        __syncthreads();
+        Cx2 Px = shfl_up_cx2(P, 1);
+        V4 ax = shfl_up_v(acc, 1);
+        if (lane == 0) { Px = ID; ax = Z4; }
+        V4 s = add4(cx2_mv(Px, S), ax);                     /* carry into this lane's run */
+        for (int64_t t = tb0; t < te0; ++t) {
+            const V4 inc = nat_ld4(agg + t * 8), r0 = nat_ld4(agg + t * 8 + 4);
+            const V4 bb = add4(r0, mv(G0, s));
+            double *cw = car + t * 8;
+            cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
+            cw[4] = bb.a; cw[5] = bb.b; cw[6] = bb.c; cw[7] = bb.d;
+            s = add4(cx2_mv(MT, s), inc);
+        }
+        /* S after the last full tile: the run holding tile Tf-1 */
+        if (Tf > 0) {
+            const int owner = (int)((Tf - 1) / CH);
+            S = V4{__shfl(s.a, owner), __shfl(s.b, owner), __shfl(s.c, owner), __shfl(s.d, owner)};
+        }
     }
     /* partial tile forward, tail, partial tile backward */
     V4 q{0, 0, 0, 0};
@@ -716,26 +767,37 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
             yd[Tf * bt + b] = dot4(Cv, q) + Dd * (dot4(Cv, Sj) + Dd * r[8]);
         }
     }
-    /* backward tile carries: car[t][4..7] = Qe_t; Q_start = M^T Qe + R0 + G0 S0 */
-    for (int64_t c1 = Tf; c1 > 0; c1 -= NC_CH) {
-        const int64_t c0 = c1 - NC_CH > 0 ? c1 - NC_CH : 0;
-        const int cn = (int)(c1 - c0);
-        for (int k = lane; k < cn * 8; k += 64) {
-            const int t = k >> 3, j = k & 7;
-            s_in[k] = j < 4 ? car[(c0 + t) * 8 + j] : agg[(c0 + t) * 8 + j];   /* S0_t | R0_t */
+    q = V4{__shfl(q.a, 0), __shfl(q.b, 0), __shfl(q.c, 0), __shfl(q.d, 0)};
+    /* backward tile carries: car[t][4..7] = Qe_t; Qe_(t-1) = M^T Qe_t + b_t.
+     * Lane l's run maps the Qe entering its last tile to the Qe leaving its
+     * first: (P, a) composed right to left; the scan runs from lane 63 down. */
+    {
+        Cx2 P = ID;
+        V4 acc = Z4;
+        for (int64_t t = te0 - 1; t >= tb0; --t) {
+            acc = add4(cx2_mv(MT, acc), nat_ld4(car + t * 8 + 4));
+            P = cx2_mul(MT, P);
         }
-        __syncthreads();
-        if (lane == 0) {
-            for (int t = cn - 1; t >= 0; --t) {
-                s_out[t * 4 + 0] = q.a; s_out[t * 4 + 1] = q.b; s_out[t * 4 + 2] = q.c; s_out[t * 4 + 3] = q.d;
-                const V4 s0{s_in[t * 8], s_in[t * 8 + 1], s_in[t * 8 + 2], s_in[t * 8 + 3]};
-                const V4 r0{s_in[t * 8 + 4], s_in[t * 8 + 5], s_in[t * 8 + 6], s_in[t * 8 + 7]};
-                q = add4(add4(mv(MT, q), r0), mv(G0, s0));
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int d = 1 << k;
+            const Cx2 Pe = shfl_down_cx2(P, d);
+            const V4 ae = shfl_down_v(acc, d);
+            if (lane + d < 64) {
+                acc = add4(cx2_mv(P, ae), acc);
+                P = cx2_mul(P, Pe);
             }
         }
-        __syncthreads();
-        for (int k = lane; k < cn * 4; k += 64) car[(c0 + k / 4) * 8 + 4 + (k & 3)] = s_out[k];
-        __syncthreads();
+        Cx2 Px = shfl_down_cx2(P, 1);
+        V4 ax = shfl_down_v(acc, 1);
+        if (lane == 63) { Px = ID; ax = Z4; }
+        V4 qq = add4(cx2_mv(Px, q), ax);                    /* Qe entering this lane's last tile */
+        for (int64_t t = te0 - 1; t >= tb0; --t) {
+            double *cw = car + t * 8;
+            const V4 bb = nat_ld4(cw + 4);
+            cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
+            qq = add4(cx2_mv(MT, qq), bb);
+        }
     }
 }
 
