@@ -27,7 +27,7 @@ OPT_ROLLQ_NOPRUNE = 16
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",
-           "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read"]
+           "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only"]
 
 
 class Params(ctypes.Structure):
@@ -88,6 +88,8 @@ def load() -> ctypes.CDLL:
     L.bpmx_profile.restype = ctypes.c_int
     L.bpmx_profile_read.argtypes = [P, ctypes.c_char_p, ctypes.c_int]
     L.bpmx_profile_read.restype = ctypes.c_int
+    L.bpmx_profile_only.argtypes = [P, ctypes.c_char_p]
+    L.bpmx_profile_only.restype = ctypes.c_int
     if L.bpmx_abi_version() != ABI_VERSION:
         raise BpmxError(f"libbpmx ABI {L.bpmx_abi_version()} != expected {ABI_VERSION}; rebuild")
     _lib = L

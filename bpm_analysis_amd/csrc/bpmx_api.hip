@@ -181,6 +181,12 @@ int bpmx_profile(bpmx_ctx *ctx, int on) {
     return BPMX_OK;
 }
 
+int bpmx_profile_only(bpmx_ctx *ctx, const char *label) {
+    if (!ctx) return fail(BPMX_E_ARG, "ctx is NULL");
+    ctx->prof_only = label ? label : "";
+    return BPMX_OK;
+}
+
 int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len) {
     if (!ctx) return fail(BPMX_E_ARG, "ctx is NULL");
     HIP_TRY(hipSetDevice(ctx->device));

@@ -40,6 +40,7 @@ struct bpmx_ctx {
     struct Rec { std::string name; hipEvent_t a, b; };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
+    std::string prof_only;              /* bpmx_profile_only: record this label only (empty: all) */
     std::map<std::string, std::pair<long, double>> totals;
 
     /* grow-only device scratch; *grew (optional) reports a fresh allocation,
@@ -78,13 +79,14 @@ struct Launch {
     hipStream_t s;
     const char *name;
     hipEvent_t a = nullptr, b = nullptr;
+    bool on() const { return ctx->prof && (ctx->prof_only.empty() || ctx->prof_only == name); }
     Launch(bpmx_ctx *c, hipStream_t st, const char *n) : ctx(c), s(st), name(n) {
-        if (ctx->prof) { a = ctx->ev(); (void)hipEventRecord(a, s); }
+        if (on()) { a = ctx->ev(); (void)hipEventRecord(a, s); }
     }
     int done() {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(BPMX_E_HIP, std::string("launch of ") + name + ": " + hipGetErrorString(e));
-        if (ctx->prof) {
+        if (on()) {
             b = ctx->ev();
             (void)hipEventRecord(b, s);
             ctx->recs.push_back({name, a, b});

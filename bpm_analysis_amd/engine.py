@@ -185,6 +185,10 @@ class Detector:
     def profile(self, on: bool):
         N.check(self.L.bpmx_profile(self.ctx, 1 if on else 0), "bpmx_profile")
 
+    def profile_only(self, label: str = ""):
+        """Restrict profiling events to launches labelled `label` ("" = all)."""
+        N.check(self.L.bpmx_profile_only(self.ctx, label.encode()), "bpmx_profile_only")
+
     def profile_read(self) -> dict:
         buf = ctypes.create_string_buffer(1 << 16)
         n = self.L.bpmx_profile_read(self.ctx, buf, len(buf))

@@ -155,6 +155,10 @@ void bpmx_synth_host(uint64_t seed, int64_t n_frames, int32_t fs, int32_t channe
  * and writes "name launches total_ms\n" lines into buf (returns bytes). */
 int bpmx_profile(bpmx_ctx *ctx, int on);
 int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len);
+/* Record events only around launches labelled `label` (NULL or "": every
+ * launch), so a timed run can carry one kernel's device time without
+ * bracketing every launch. */
+int bpmx_profile_only(bpmx_ctx *ctx, const char *label);
 
 #ifdef __cplusplus
 }
