@@ -428,7 +428,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             }
             return BPMX_OK;
         };
-        const dim3 g2((unsigned)((maxnd + 255) / 256), F);
+        const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, 8), F);
         if (O->n_raw_troughs)
             HIP_TRY(hipMemcpyAsync(O->n_raw_troughs, d_nraw, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
         {

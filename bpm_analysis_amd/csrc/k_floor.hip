@@ -36,13 +36,13 @@ __global__ __launch_bounds__(256) void k_interp(InterpArgs A) {
     const int f = blockIdx.y;
     if (f >= A.n_files || !A.run[f]) return;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
-    const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (x >= n) return;
     if (n <= A.skip_n && A.ntr[f] <= WM_TRMAX) return;      /* k_rollq_wm interpolates these itself */
     const int64_t *t = A.troughs + d0;
     const double *e = A.env + d0;
-    const double r = interp_at(x, t, [&](int j) { return e[t[j]]; }, A.ntr[f]);
-    A.dense[d0 + x] = r;
+    /* a few workgroups per recording striding over it: a recording the
+     * rolling-quantile kernel interpolates itself costs one early exit */
+    for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256)
+        A.dense[d0 + x] = interp_at(x, t, [&](int j) { return e[t[j]]; }, A.ntr[f]);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -507,23 +507,25 @@ __global__ __launch_bounds__(256) void k_floor_final(FinalArgs A) {
     const int f = blockIdx.y;
     if (f >= A.n_files || !A.active[f]) return;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int fl = A.flags[f];
     const double *qv = A.qv + (int64_t)f * Q_SLOTS;
-    bool nanfb = false;
-    double v;
+    bool nanfb = false, from_draft = false;
+    double v = 0.0;
     if (fl & BPMX_F_STATIC_FLOOR) {
         v = qv[Q_NOISE];
     } else if (fl & BPMX_F_DRAFT_FLOOR) {
         nanfb = A.allnan_draft[f] != 0;
-        v = nanfb ? qv[Q_FALLBACK] : (i < n ? A.draft[d0 + i] : 0.0);
+        from_draft = !nanfb;
+        v = qv[Q_FALLBACK];
     } else {
         nanfb = A.allnan_final[f] != 0;
         if (!nanfb) return;   /* floor already written by the second rolling pass */
         v = qv[Q_FALLBACK];
     }
-    if (i < n) A.floor[d0 + i] = v;
-    if (i == 0 && nanfb) A.flags[f] = fl | BPMX_F_NAN_FLOOR;
+    /* a few workgroups per recording striding over it */
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        A.floor[d0 + i] = from_draft ? A.draft[d0 + i] : v;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nanfb) A.flags[f] = fl | BPMX_F_NAN_FLOOR;
 }
 
 }  // namespace bpmx
