@@ -159,6 +159,39 @@ def reduce_results(elapsed: float, n_peaks, world: int, rank: int):
     return float(tt.item()), total
 
 
+def peak_slab(peaks, doff, counts):
+    """Per-file raw-peak indices as a padded [files, cap] int32 slab (-1 pads):
+    the fixed-size record each shard hands to the final result gather."""
+    import torch
+    cap = int(counts.max().item()) if counts.numel() else 0
+    cap = max(cap, 1)
+    ar = torch.arange(cap, device=peaks.device, dtype=torch.int64)
+    start = doff[:-1].to(peaks.device).unsqueeze(1)
+    idx = (start + ar.unsqueeze(0)).clamp(max=peaks.numel() - 1)
+    slab = peaks[idx].to(torch.int32)
+    return torch.where(ar.unsqueeze(0) < counts.to(peaks.device).long().unsqueeze(1), slab,
+                       torch.full_like(slab, -1))
+
+
+def gather_peak_slabs(slab, world: int, rank: int):
+    """The final result gather: every shard's padded peak slab to
+    rank 0 over RCCL (gloo in the CPU tests); slabs are padded to the widest
+    shard first.  Returns the list of slabs on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    if world <= 1:
+        return [slab]
+    w = torch.tensor([slab.shape[1]], dtype=torch.int64, device=slab.device)
+    dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    cap = int(w.item())
+    if slab.shape[1] < cap:
+        pad = torch.full((slab.shape[0], cap - slab.shape[1]), -1, dtype=slab.dtype, device=slab.device)
+        slab = torch.cat([slab, pad], dim=1)
+    out = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
+    dist.gather(slab.contiguous(), out, dst=0)
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -215,6 +248,12 @@ def main():
     det.profile(False)
     prof = det.profile_read()
     elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
+    slabs = gather_peak_slabs(peak_slab(out.peaks, torch.from_numpy(out.doff), out.n_peaks), world, rank)
+    gathered = None
+    if rank == 0:
+        gathered = {"ranks": len(slabs), "files": int(sum(s.shape[0] for s in slabs)),
+                    "bytes": int(sum(s.numel() * 4 for s in slabs)),
+                    "peaks": int(sum(int((s >= 0).sum()) for s in slabs))}
     # per-kernel table from a separate, untimed pass with every launch bracketed
     det.profile_only("")
     det.profile(True)
@@ -290,6 +329,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
+            "result_gather": gathered,
         }
         print(json.dumps(line))
     if world > 1:

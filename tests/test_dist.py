@@ -21,7 +21,16 @@ def _worker(rank, world, port, q):
     import bench
     counts = torch.arange(4, dtype=torch.int32) + 10 * rank      # per-file peak counts of this shard
     elapsed, total = bench.reduce_results(1.0 + rank, counts, world, rank)
-    q.put((rank, elapsed, total, bench.shard_seed0(rank, 4)))
+    # padded peak slabs: file f of rank r holds peaks 100*r + f*1000 + [0, counts[f])
+    doff = torch.tensor([0, 50, 100, 150, 200], dtype=torch.int64)
+    peaks = torch.full((200,), -7, dtype=torch.int64)
+    for f in range(4):
+        peaks[doff[f]:doff[f] + counts[f]] = 100 * rank + 1000 * f + torch.arange(int(counts[f]))
+    slabs = bench.gather_peak_slabs(bench.peak_slab(peaks, doff, counts), world, rank)
+    summary = None
+    if rank == 0:
+        summary = [[row[row >= 0].tolist() for row in s] for s in slabs]
+    q.put((rank, elapsed, total, bench.shard_seed0(rank, 4), summary))
     dist.destroy_process_group()
 
 
@@ -36,7 +45,12 @@ def test_two_rank_gather_and_max_time():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, e0, t0, s0), (r1, e1, t1, s1) = res
+    (r0, e0, t0, s0, g0), (r1, e1, t1, s1, g1) = res
+    assert g1 is None and len(g0) == 2
+    for r in range(2):
+        for f in range(4):
+            n = f + 10 * r
+            assert g0[r][f] == [100 * r + 1000 * f + k for k in range(n)]
     assert e0 == e1 == 2.0                        # max over ranks
     assert t0 == (0 + 1 + 2 + 3) + (10 + 11 + 12 + 13) and t1 == 0
     assert (s0, s1) == (0, 4)                     # disjoint synthetic shards
