@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=3, help="steps of the PCIe-inclusive side measurement (0: skip)")
     ap.add_argument("--options", type=int, default=0, help="bpmx_option bits (diagnostics; 0 = defaults)")
+    ap.add_argument("--contexts", type=int, default=4,
+                    help="side measurement: the batch split over K contexts on K streams (0: skip)")
     return ap.parse_args()
 
 
@@ -282,6 +284,39 @@ def main():
                 "h2d_bytes_per_step": F * n * 2, "steps": args.pcie_steps, "per_gpu": True}
         del host, stream
 
+    # Side measurement (never `value`): the same batch as K sub-batches on K
+    # library contexts and K streams, so the latency-bound per-recording
+    # kernels of one sub-batch fill the tails of another's.
+    multi = None
+    if args.contexts > 1 and F % args.contexts == 0:
+        K, per = args.contexts, F // args.contexts
+        dets = [det] + [Detector(local) for _ in range(K - 1)]
+        streams = [torch.cuda.Stream(det.device) for _ in range(K)]
+        fok = np.arange(per + 1, dtype=np.int64) * n
+        outs = [dets[k].alloc(fok, d.ds, d.sr) for k in range(K)]
+        views = [pcm[k * per * n:(k + 1) * per * n] for k in range(K)]
+
+        def mstep():
+            for k in range(K):
+                with torch.cuda.stream(streams[k]):
+                    dets[k].run(views[k], fok, fs, params, mode=args.mode, out=outs[k], d=d, options=args.options)
+
+        for _ in range(2):
+            mstep()
+        torch.cuda.synchronize()
+        tm0 = time.perf_counter()
+        msteps = max(3, min(args.steps, 10))
+        for _ in range(msteps):
+            mstep()
+        torch.cuda.synchronize()
+        mdt = (time.perf_counter() - tm0) / msteps
+        multi = {"contexts": K, "value": F * n / mdt, "unit": "audio-samples/s", "ms_per_step": mdt * 1e3,
+                 "steps": msteps, "per_gpu": True,
+                 "peaks_match": int(sum(int(o.n_peaks.sum()) for o in outs)) == int(out.n_peaks.sum())}
+        for x in dets[1:]:
+            x.close()
+        del outs, views, streams
+
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         value = world * F * n / (elapsed / args.steps)
@@ -329,7 +364,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
-            "result_gather": gathered,
+            "result_gather": gathered, "multi_context": multi,
         }
         print(json.dumps(line))
     if world > 1:
