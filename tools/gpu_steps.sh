@@ -19,12 +19,12 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_ref) run bench_ref 600 python bench.py --steps 10 --warmup 2 --mode reference ;;
-    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
-    rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --mode reference ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
-    pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --mode reference ;;
-    pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --mode reference ;;
+    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 ;;
+    rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --mode reference ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 ;;
+    pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --mode reference ;;
+    pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --mode reference ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
