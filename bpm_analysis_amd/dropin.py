@@ -8,7 +8,8 @@ pixeru/bpm_analysis (bpm_analysis.py):
 * ``find_raw_peaks(env, sr, params, height_threshold) -> peaks``          :223-229
   (the body of ``PeakClassifier._find_raw_peaks``)
 
-plus the batch entry points the reference lacks (``analyze_batch``) and
+plus the batch entry points the reference lacks (``analyze_batch``,
+``analyze_wav_files``) and
 ``patch_reference(module)``, which rebinds an imported reference module's
 three hot-path functions to these so its unchanged ``analyze_wav_file``
 (and therefore gui.py / main.py / the Gradio app) runs on the GPU.
@@ -118,6 +119,58 @@ def analyze_batch(recordings: Sequence[np.ndarray], fs: int, params: Dict, mode:
     """
     design(fs, params)   # Nyquist check / clamp warnings once per batch
     return default_detector(device).run_host(list(recordings), fs, params, mode=mode, stages=N.STAGE_ALL)
+
+
+def analyze_wav_files(file_paths: Sequence[str], params: Dict, output_directory: str, mode: str = None,
+                      device: int = 0) -> List[dict]:
+    """Batched file entry point: what ``preprocess_audio`` + the noise floor +
+    the raw-peak call do per file (bpm_analysis.py:1007-1062, :1064-1117,
+    :223-229), for many WAV files in few launch sequences.
+
+    Files are read with ``scipy.io.wavfile`` (the reference's dtype rules:
+    u8 / i16 / i32 (PCM24 and PCM32) / f32 / f64, stereo averaged on the
+    device), grouped by (sample rate, sample format, channels) and run as one
+    ragged batch per group.  With ``params["save_filtered_wav"]`` both debug
+    WAVs of the reference are written (next to the input and into
+    ``output_directory``).  Returns one dict per path, in order: env, floor,
+    troughs, peaks, sr, flags, or ``error`` (the exception the reference would
+    raise for that file, e.g. the filtfilt padlen ValueError)."""
+    if mode is None:
+        mode = params.get("bpmx_mode", "reference")
+    save = bool(params.get("save_filtered_wav", False))
+    out: List[dict] = [None] * len(file_paths)
+    groups: Dict[tuple, List[int]] = {}
+    audio = []
+    for k, path in enumerate(file_paths):
+        try:
+            fs, a = _read_wav(path)
+        except Exception as exc:                      # wavfile errors propagate per file, as in the GUI loop
+            out[k] = {"error": exc}
+            audio.append(None)
+            continue
+        audio.append((fs, a))
+        key = (fs, a.dtype.str, 1 if a.ndim == 1 else a.shape[1])
+        groups.setdefault(key, []).append(k)
+    det = default_detector(device)
+    for (fs, _, _), idx in groups.items():
+        try:
+            d = design(fs, params)                    # clamp warnings / Nyquist ValueError, once per group
+        except ValueError as exc:
+            for k in idx:
+                out[k] = {"error": exc}
+            continue
+        res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save)
+        for k, r in zip(idx, res):
+            if r["flags"] & N.F_TOO_SHORT:
+                out[k] = {"error": ValueError(PADLEN_MSG)}
+                continue
+            if save:
+                path = file_paths[k]
+                _write_debug_wav(f"{os.path.splitext(path)[0]}_filtered_debug.wav", d.sr, r["y"])
+                base = os.path.basename(os.path.splitext(path)[0])
+                _write_debug_wav(os.path.join(output_directory, f"{base}_filtered_debug.wav"), d.sr, r["y"])
+            out[k] = {key: r[key] for key in ("env", "floor", "troughs", "peaks", "sr", "flags")}
+    return out
 
 
 def patch_reference(module) -> None:

@@ -216,6 +216,39 @@ def test_config_c5_96k_stereo_ragged(det):
         _check_file(h, o, exact_env=False)
 
 
+def test_analyze_wav_files_batched_ingest(det, tmp_path):
+    """WAV files of mixed formats in one call — grouped by
+    (rate, format, channels), each group one ragged batch — against the
+    oracle bit for bit (reference mode), both debug WAVs as the reference
+    writes them, and the padlen ValueError for a too-short file."""
+    from scipy.io import wavfile
+    from bpm_analysis_amd import dropin
+    params = dict(G.BASE_PARAMS, save_filtered_wav=True)
+    cases = [("a_i16.wav", 44100, O.synth(31, 44100 * 20, 44100, 1)),
+             ("b_i16_stereo.wav", 48000, O.synth(32, 48000 * 15, 48000, 2)),
+             ("c_f32.wav", 44100, (O.synth(33, 44100 * 12, 44100, 1) / 32768.0).astype(np.float32)),
+             ("d_i16.wav", 44100, O.synth(34, 44100 * 9 + 5, 44100, 1)),
+             ("e_short.wav", 44100, O.synth(35, 146 * 15, 44100, 1))]
+    paths = []
+    for name, fs, pcm in cases:
+        paths.append(str(tmp_path / name))
+        wavfile.write(paths[-1], fs, pcm)
+    outdir = tmp_path / "out"
+    outdir.mkdir()
+    res = dropin.analyze_wav_files(paths, params, str(outdir), mode="reference")
+    for (name, fs, pcm), path, r in zip(cases, paths, res):
+        if name.startswith("e_"):
+            assert isinstance(r["error"], ValueError) and "padlen" in str(r["error"])
+            continue
+        o = O.detect(wavfile.read(path)[1], fs, params, mode="reference")
+        assert _same(r["env"], o["env"]) and _same(r["floor"], o["floor"])
+        assert _same(r["troughs"], o["troughs"]) and _same(r["peaks"], o["peaks"])
+        want = np.int16(o["y"] / np.max(np.abs(o["y"])) * 32767)
+        for dbg in (path[:-4] + "_filtered_debug.wav", str(outdir / (name[:-4] + "_filtered_debug.wav"))):
+            sr, got = wavfile.read(dbg)
+            assert sr == o["sr"] and _same(got, want)
+
+
 def test_reference_side_ctypes_stub():
     """INTEGRATION.md's torch-free ctypes binding of the C ABI, on a golden."""
     import importlib.util
