@@ -534,6 +534,10 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     /* the kept candidates are taken NP at a time per wave so that their global
      * loads overlap */
     constexpr int NP = BPMX_FP_NP;
+#ifdef BPMX_STAMPS
+    __shared__ unsigned long long s_wt_prom[FP_T / 64];
+    const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
     {
         const int nw = FP_T / 64, wv = wave_id();
         int j = wv;
@@ -558,8 +562,19 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
             }
         }
     }
+#ifdef BPMX_STAMPS
+    if (lane_id() == 0) s_wt_prom[wave_id()] = __builtin_amdgcn_s_memtime() - tp0;
+#endif
     __syncthreads();
     STAMP(3);
+#ifdef BPMX_STAMPS
+    if (threadIdx.x == 0) {
+        unsigned long long mx = 0, sm = 0;
+        for (int w = 0; w < FP_T / 64; ++w) { mx = s_wt_prom[w] > mx ? s_wt_prom[w] : mx; sm += s_wt_prom[w]; }
+        _st_acc[5] += mx;
+        _st_acc[6] += sm / (FP_T / 64);
+    }
+#endif
 
     /* (5) ordered compaction */
     int64_t *out = A.out + d0;

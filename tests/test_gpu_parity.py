@@ -216,6 +216,26 @@ def test_config_c5_96k_stereo_ragged(det):
         _check_file(h, o, exact_env=False)
 
 
+def test_config_c5_full_length_recording(det):
+    """BASELINE config C5 at its maximum size: one 30-min 96 kHz stereo
+    recording (172.8 M frames, 691 MB of PCM, Nd = 576,000: rocFFT Hilbert
+    fallback, sorted-union rolling quantile, global find_peaks tables)."""
+    import torch
+    fs, n = 96000, 96000 * 1800
+    fo = np.array([0, n], dtype=np.int64)
+    dev = det.synth(fo, fs, 2, seed0=777)
+    params = dict(G.BASE_PARAMS)
+    res = det.run(dev, fo, fs, params, mode="native", channels=2, want_y=True)
+    torch.cuda.synchronize()
+    h = res.to_host()[0]
+    del dev
+    o = O.detect(O.synth(777, n, fs, 2), fs, params, mode="native")
+    assert h["sr"] == o["sr"] == 320 and len(h["env"]) == 576000
+    scale = np.max(np.abs(o["y"]))
+    assert np.max(np.abs(h["y"] - o["y"])) <= 1e-9 * scale
+    _check_file(h, o, exact_env=False)
+
+
 def test_analyze_wav_files_batched_ingest(det, tmp_path):
     """WAV files of mixed formats in one call — grouped by
     (rate, format, channels), each group one ragged batch — against the

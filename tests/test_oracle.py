@@ -1,4 +1,6 @@
 """The CPU oracle against the reference's golden vectors (pins the oracle)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -67,3 +69,27 @@ def test_short_input_raises():
     pcm = O.synth(1, 146 * 15, 44100, 1)
     with pytest.raises(ValueError):
         O.detect(pcm, 44100, G.BASE_PARAMS)
+
+
+def test_oracle_under_sanitizers(tmp_path):
+    """SURVEY.md section 5 (race detection / sanitizers): the C restatement under
+    ASan + UBSan on synthetic recordings (reference and native ordering,
+    stereo, padlen rejects) and envelope edge cases (constant, ramps, windows
+    longer than the recording).  Any invalid access, leak or UB fails."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc")
+    if cc is None:
+        pytest.skip("gcc not available")
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "sanitize_driver")
+    cmd = [cc, "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1",
+           "-ffp-contract=off", "-std=c11", "-o", exe, os.path.join(here, "sanitize_driver.c"), "-lm"]
+    b = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if b.returncode != 0 and "sanitize" in (b.stderr or ""):
+        pytest.skip("sanitizer runtime not available: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "SANITIZE OK" in r.stdout

@@ -86,7 +86,7 @@ int main(int argc, char **argv) {
         for (int k = 0; k < 8; ++k) tot += sum[k];
         long long np = 0;
         for (auto v : no) np += v;
-        const char *names[8] = {"tables", "maxima", "distance", "prominence", "compact", "-", "-", "-"};
+        const char *names[8] = {"tables", "maxima", "distance", "prominence", "compact", "(prom max wave)", "(prom mean wave)", "-"};
         printf("sign %+.0f: %.3f ms, %lld peaks; per-WG cycles %.0f\n", sg, best, np, tot / F);
         for (int k = 0; k < 8; ++k)
             if (sum[k] > 0) printf("   %-11s %10.0f  %5.1f%%\n", names[k], sum[k] / F, 100 * sum[k] / tot);
