@@ -401,3 +401,43 @@ def test_draft_bounds_match_full_draft(det, name):
         assert _same(r["troughs"], g["troughs"])
         assert (r["flags"] & 7) == int(g["flags"])
         assert _same(r["peaks"], g["peaks"])
+
+
+def test_beat_stages_on_gpu_outputs(tmp_path):
+    """the host beat stages (classifier, refinement,
+    BPM curve, slopes/HRR/HRV) on the GPU path's outputs of a batched run, against
+    goldens made by the reference (tests/golden/beats); the long recordings are
+    regenerated PCM, so everything upstream of the classifier ran on the GPU."""
+    import json
+    from scipy.io import wavfile
+    from bpm_analysis_amd import beats as B, dropin
+    from tests import test_beats as TB
+    from tests.golden import inputs as I
+    names = ["long_6k_8min", "long_8k_5min_hint"]
+    for name in names:
+        g, params, hint, _ = TB.load_case(name)
+        spec = json.loads(str(g["spec"]))
+        pcm, fs = I.make_input(spec)
+        r = dropin.analyze_batch([pcm], fs, params, mode="reference")[0]
+        assert np.array_equal(r["peaks"], g["all_raw_peaks"])
+        res = B.analyze_many([r], params, hint)[0]
+        TB.check_against_golden(g, res)
+        # the reference entry point end to end: WAV in, <base>_bpm_plot.csv out
+        wav = tmp_path / f"{name}.wav"
+        wavfile.write(str(wav), fs, pcm)
+        p = dict(params, save_filtered_wav=False)
+        assert B.analyze_wav_file(str(wav), p, hint, str(wav), str(tmp_path)) is None
+        assert (tmp_path / f"{name}_bpm_plot.csv").read_text() == str(g["csv"])
+
+
+def test_beat_stages_batch_of_hot_path_goldens():
+    """Every regenerable hot-path golden in one ragged GPU batch per rate, then
+    the beat stages per file against the reference's beat goldens."""
+    from bpm_analysis_amd import beats as B, dropin
+    from tests import test_beats as TB
+    for name in ["ref_44k_60s_mono", "ref_44k_60s_mono_hint", "ref_44k_40s_clicks", "ref_44k_20s_wrap"]:
+        g, params, hint, inp = TB.load_case(name)
+        h = G.load(str(g["source"]))
+        r = dropin.analyze_batch([h["pcm"]], int(h["fs"]), params, mode="reference")[0]
+        assert np.array_equal(r["env"], inp["env"]) and np.array_equal(r["peaks"], inp["peaks"])
+        TB.check_against_golden(g, B.analyze_many([r], params, hint)[0])
