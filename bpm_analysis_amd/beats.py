@@ -612,16 +612,21 @@ def analyze_wav_file(wav_file_path: str, params: Dict, start_bpm_hint: Optional[
                      output_directory: str, mode: Optional[str] = None, device: int = 0):
     """The reference entry point (:1725) on the GPU path: preprocess + floor + raw
     peaks in one batched run, then the host stages above; writes the filtered
-    debug WAVs and ``<base>_bpm_plot.csv``.  The HTML plot and markdown reports
-    (Plotter / ReportGenerator) are not produced.  Returns None."""
+    debug WAVs, ``<base>_bpm_plot.csv`` and the ReportGenerator files
+    (reports.py: summary, debug log, settings).  The interactive HTML plot
+    (Plotter's plotly figure) is not produced.  Returns None."""
     from .dropin import analyze_wav_files
     r = analyze_wav_files([wav_file_path], params, output_directory, mode=mode, device=device)[0]
     if "error" in r:
         raise r["error"]
     res = analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], r["peaks"], params, start_bpm_hint)
-    if res["final_metrics"] is not None:
+    m = res["final_metrics"]
+    if m is not None:
+        from .reports import write_reports
         base = os.path.basename(os.path.splitext(original_file_path)[0])
-        write_bpm_csv(os.path.join(output_directory, f"{base}_bpm_plot.csv"), res["final_metrics"])
+        write_bpm_csv(os.path.join(output_directory, f"{base}_bpm_plot.csv"), m)
+        write_reports(original_file_path, output_directory, np.asarray(r["env"], dtype=np.float64), r["sr"],
+                      res["all_raw_peaks"], res["analysis_data"], m, start_bpm_hint)
     return None
 
 

@@ -8,7 +8,8 @@ two long synthetic recordings (regenerated bit-exactly by
 reference's stages 2-6 of ``analyze_wav_file`` (bpm_analysis.py:1734-1757):
 ``_run_preliminary_pass`` (:1623), ``PeakClassifier.classify_peaks`` (:113),
 ``_refine_and_correct_peaks`` (:1655), ``_calculate_final_metrics`` (:1701),
-and the BPM CSV written by ``Plotter.plot_and_save`` (:458-473).  It records
+the BPM CSV written by ``Plotter.plot_and_save`` (:458-473) and the
+``ReportGenerator`` files (summary, debug log, settings; :782-985).  It records
 the outputs as data in ``tests/golden/beats/<name>.npz``.
 
     python tests/golden/make_beat_goldens.py
@@ -104,6 +105,18 @@ def run_case(name, env, sr, floor, troughs, params, hint):
         p.plot_and_save(env, raw, data, m)
         csv_path = os.path.join(td, name + "_bpm_plot.csv")
         out["csv"] = open(csv_path).read() if os.path.exists(csv_path) else ""
+        # ReportGenerator (:782-985); the one timestamp line of each markdown file is dropped
+        rep = R.ReportGenerator(os.path.join(td, name + ".wav"), td)
+        rep.save_analysis_summary(m)
+        rep.create_chronological_log(env, sr, raw, data, m)
+        rep.save_analysis_settings(hint)
+        for key, suffix in (("summary_md", "_Analysis_Summary.md"), ("debug_log_md", "_Debug_Log.md"),
+                            ("settings_json", "_Analysis_Settings.json")):
+            text = open(os.path.join(td, name + suffix), encoding="utf-8").read()
+            if suffix.endswith(".md"):
+                lines = text.split("\n")
+                text = "\n".join(lines[:1] + lines[2:])
+            out[key] = text
     return out
 
 

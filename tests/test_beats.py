@@ -150,3 +150,26 @@ def test_update_long_term_bpm_limits():
     assert B.update_long_term_bpm(0.5, 80.0, p) == pytest.approx(81.5)          # EMA says 82, slew limit 3 * 0.5
     assert B.update_long_term_bpm(0.1, 80.0, p) == pytest.approx(80.3)          # slew-limited to 3 * 0.1
     assert B.update_long_term_bpm(10.0, p["min_bpm"], p) == p["min_bpm"]         # clamped
+
+
+def _drop_stamp(text: str) -> str:
+    lines = text.split("\n")
+    return "\n".join(lines[:1] + lines[2:])
+
+
+@pytest.mark.parametrize("name", [c for c in CASES])
+def test_reports_match_reference(name, tmp_path):
+    """Analysis_Summary.md, Debug_Log.md (minus the timestamp line) and
+    Analysis_Settings.json byte-equal to the reference's ReportGenerator."""
+    from bpm_analysis_amd import reports as RP
+    g, params, hint, inp = load_case(name)
+    if "summary_md" not in g:
+        pytest.skip("the reference writes no reports for this case")
+    res = B.analyze_recording(inp["env"], inp["sr"], inp["floor"], inp["troughs"], inp["peaks"], params, hint)
+    fname = os.path.join(str(tmp_path), name + ".wav")
+    RP.write_reports(fname, str(tmp_path), inp["env"], inp["sr"], res["all_raw_peaks"], res["analysis_data"],
+                     res["final_metrics"], hint)
+    got = lambda suffix: (tmp_path / (name + suffix)).read_text(encoding="utf-8")  # noqa: E731
+    assert _drop_stamp(got("_Analysis_Summary.md")) == str(g["summary_md"])
+    assert _drop_stamp(got("_Debug_Log.md")) == str(g["debug_log_md"])
+    assert got("_Analysis_Settings.json") == str(g["settings_json"])

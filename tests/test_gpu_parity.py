@@ -428,6 +428,9 @@ def test_beat_stages_on_gpu_outputs(tmp_path):
         p = dict(params, save_filtered_wav=False)
         assert B.analyze_wav_file(str(wav), p, hint, str(wav), str(tmp_path)) is None
         assert (tmp_path / f"{name}_bpm_plot.csv").read_text() == str(g["csv"])
+        assert TB._drop_stamp((tmp_path / f"{name}_Analysis_Summary.md").read_text()) == str(g["summary_md"])
+        assert TB._drop_stamp((tmp_path / f"{name}_Debug_Log.md").read_text()) == str(g["debug_log_md"])
+        assert (tmp_path / f"{name}_Analysis_Settings.json").read_text() == str(g["settings_json"])
 
 
 def test_beat_stages_batch_of_hot_path_goldens():
