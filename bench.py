@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-files", type=int, default=-1, help="CPU baseline sample size (-1: auto, 0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pcie-steps", type=int, default=3, help="steps of the PCIe-inclusive side measurement (0: skip)")
+    ap.add_argument("--host-beat-files", type=int, default=16,
+                    help="files of the side measurement of the host beat stages (0: skip)")
     ap.add_argument("--options", type=int, default=0, help="bpmx_option bits (diagnostics; 0 = defaults)")
     ap.add_argument("--contexts", type=int, default=4,
                     help="side measurement: the batch split over K contexts on K streams (0: skip)")
@@ -317,6 +319,20 @@ def main():
             x.close()
         del outs, views, streams
 
+    # Side measurement (never `value`): the host beat stages (beats.py: classifier,
+    # refinement, BPM curve, metrics — SURVEY 8(f) rows 1 and 3) on the first
+    # files of this batch's GPU outputs, one core.  Outside the north-star metric.
+    host_beats = None
+    if rank == 0 and args.host_beat_files > 0:
+        from bpm_analysis_amd import beats
+        res = out.to_host()[:args.host_beat_files]
+        th0 = time.perf_counter()
+        done = beats.analyze_many(res, params)
+        hdt = time.perf_counter() - th0
+        host_beats = {"files": len(res), "cores": 1, "files_per_s": len(res) / hdt,
+                      "audio_samples_per_s": len(res) * n / hdt, "ms_per_file": hdt / len(res) * 1e3,
+                      "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))}
+
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         value = world * F * n / (elapsed / args.steps)
@@ -364,7 +380,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
-            "result_gather": gathered, "multi_context": multi,
+            "result_gather": gathered, "multi_context": multi, "host_beat_stages": host_beats,
         }
         print(json.dumps(line))
     if world > 1:
