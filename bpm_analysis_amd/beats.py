@@ -23,6 +23,7 @@ Parity: tests/test_beats.py against goldens made by the reference itself
 """
 from __future__ import annotations
 
+import bisect
 import csv
 import datetime
 import logging
@@ -46,29 +47,65 @@ S2_GAP = "S2 (Paired - Corrected from Gap)"
 # reference's substring tests on the debug strings, which are unique per tag)
 _T_NONE, _T_S1, _T_S2, _T_LONE, _T_NOISE = 0, 1, 2, 3, 4
 
-_DEV_X = np.array([0.0, 0.25, 0.40, 0.80, 1.0])
-_CURVE_LO = np.array([0.9, 0.9, 0.7, 0.1, 0.1])
-_CURVE_HI = np.array([0.1, 0.5, 0.75, 0.65, 0])
-_RHYTHM_X, _RHYTHM_Y = [0.0, 0.15, 0.30, 0.50], [1.0, 0.8, 0.4, 0.0]
-_AMP_X, _AMP_Y = [0.0, 0.4, 0.7, 1.0], [0.0, 0.4, 0.8, 1.0]
+_DEV_X = (0.0, 0.25, 0.40, 0.80, 1.0)
+_CURVE_LO = (0.9, 0.9, 0.7, 0.1, 0.1)
+_CURVE_HI = (0.1, 0.5, 0.75, 0.65, 0.0)
+_RHYTHM_X, _RHYTHM_Y = (0.0, 0.15, 0.30, 0.50), (1.0, 0.8, 0.4, 0.0)
+_AMP_X, _AMP_Y = (0.0, 0.4, 0.7, 1.0), (0.0, 0.4, 0.8, 1.0)
+
+
+# Scalar numpy.interp / numpy.clip on Python floats: the same IEEE operations in
+# the same order as numpy's compiled loops (numpy/_core/src/multiarray/
+# compiled_base.c arr_interp: bracket by binary search, exact hits and the right
+# end return fp[j], else slope*(x - xp[j]) + fp[j], NaN retried from the right
+# end), without numpy's per-call overhead on the classifier's hot loop.
+def _interp(x, xp, fp):
+    if x != x:
+        return x
+    if x < xp[0]:
+        return fp[0]
+    n = len(xp)
+    if x > xp[n - 1]:
+        return fp[n - 1]
+    j = bisect.bisect_right(xp, x) - 1
+    if j == n - 1 or xp[j] == x:
+        return fp[j]
+    slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j])
+    r = slope * (x - xp[j]) + fp[j]
+    if r != r:
+        r = slope * (x - xp[j + 1]) + fp[j + 1]
+        if r != r and fp[j] == fp[j + 1]:
+            r = fp[j]
+    return r
+
+
+def _clip(x, lo, hi):
+    """numpy.clip for scalars: NaN propagates, ties keep x (so -0.0 stays -0.0)."""
+    if x != x:
+        return x
+    if x < lo:
+        return float(lo)
+    if x > hi:
+        return float(hi)
+    return x
 
 
 # ---------------------------------------------------------------- confidence models
 def _blend(bpm: float, p: Dict):
-    return np.clip((bpm - p['contractility_bpm_low']) / (p['contractility_bpm_high'] - p['contractility_bpm_low']), 0, 1)
+    return _clip((bpm - p['contractility_bpm_low']) / (p['contractility_bpm_high'] - p['contractility_bpm_low']), 0, 1)
 
 
 def calculate_blended_confidence(deviation: float, bpm: float, params: Dict) -> float:
     """Pairing confidence from the amplitude deviation on a BPM-blended curve (:1120-1143)."""
     b = _blend(bpm, params)
-    return np.interp(deviation, _DEV_X, _CURVE_LO + (_CURVE_HI - _CURVE_LO) * b)
+    return _interp(deviation, _DEV_X, tuple(lo + (hi - lo) * b for lo, hi in zip(_CURVE_LO, _CURVE_HI)))
 
 
 def update_long_term_bpm(new_rr_sec: float, current_long_term_bpm: float, params: Dict) -> float:
     """EMA (lr 0.05) with a 3 BPM-per-second-of-RR slew limit, clamped to [min_bpm, max_bpm] (:1239-1255)."""
     target = (1 - 0.05) * current_long_term_bpm + 0.05 * (60.0 / new_rr_sec)
     lim = 3.0 * new_rr_sec
-    step = np.clip(target - current_long_term_bpm, -lim, lim)
+    step = _clip(target - current_long_term_bpm, -lim, lim)
     return max(params['min_bpm'], min(current_long_term_bpm + step, params['max_bpm']))
 
 
@@ -107,47 +144,51 @@ class PeakClassifier:
         win = max(5, int(len(dev) * p['deviation_smoothing_factor']))
         self._dev = pd.Series(dev).rolling(window=win, min_periods=1, center=True).mean().to_numpy()
         self.deviation_series = pd.Series(self._dev, index=self._dev_t)
+        # per raw peak, as Python floats for the sequential loop (same IEEE values)
+        self._pkl = pk.tolist()
+        self._envpk = env[pk].tolist()
+        self._str = [max(0, e - f) for e, f in zip(self._envpk, floor[pk].tolist())]
+        self._devl, self._dev_tl = self._dev.tolist(), self._dev_t.tolist()
         self.start_bpm = float(start_bpm_hint) if start_bpm_hint else 80.0
 
     # -- helpers --------------------------------------------------------
     def _dev_asof(self, t: float) -> float:
         """Series.asof on the smoothed deviations: last non-NaN value at index <= t."""
-        k = int(np.searchsorted(self._dev_t, t, side="right")) - 1
-        while k >= 0 and np.isnan(self._dev[k]):
+        d = self._devl
+        k = bisect.bisect_right(self._dev_tl, t) - 1
+        while k >= 0 and d[k] != d[k]:
             k -= 1
-        return self._dev[k] if k >= 0 else np.nan
+        return d[k] if k >= 0 else float("nan")
 
-    def _strength(self, i: int):
-        return max(0, self.audio_envelope[i] - self._floor[i])
-
-    def _pair(self, s1: int, s2: int, ratio: float, ltb: float, n_beats: int) -> Tuple[bool, str]:
-        """Pairing decision for raw peaks s1 < s2 (:231-272, :1146-1197)."""
+    def _pair(self, j: int, ratio: float, ltb: float, n_beats: int) -> Tuple[bool, str]:
+        """Pairing decision for raw peaks #j and #j+1 (:231-272, :1146-1197)."""
         p, sr = self.params, self.sample_rate
+        s1, s2 = self._pkl[j], self._pkl[j + 1]
         gap = (s2 - s1) / sr
         conf = calculate_blended_confidence(self._dev_asof(s1 / sr), ltb, p)
         why = f"Base Conf (Blended Model {_blend(ltb, p):.0%} High): {conf:.2f}"
         if n_beats >= 5:
-            f = np.interp(ratio, [0.0, 1.0], [p.get("stability_confidence_floor", 0.85),
-                                             p.get("stability_confidence_ceiling", 1.10)])
+            f = _interp(ratio, (0.0, 1.0), (p.get("stability_confidence_floor", 0.85),
+                                            p.get("stability_confidence_ceiling", 1.10)))
             conf *= f
             why += f"\n- Stability Pre-Adjust: x{f:.2f} (Pairing Ratio: {ratio:.0%})"
-        a1, a2 = self._strength(s1), self._strength(s2)
+        a1, a2 = self._str[j], self._str[j + 1]
         r21 = a2 / (a1 + 1e-9)
         lo = p['contractility_bpm_low']
         t1, t2 = self.peak_bpm_time_sec, self.recovery_end_time_sec
         recovering = t1 is not None and t2 is not None and t1 < (s1 / sr) < t2
-        r_max = np.interp(max(ltb, lo) if recovering else ltb, [lo, p['contractility_bpm_high']],
-                          [p['s2_s1_ratio_low_bpm'], p['s2_s1_ratio_high_bpm']])
+        r_max = np.float64(_interp(max(ltb, lo) if recovering else ltb, (lo, p['contractility_bpm_high']),
+                                   (p['s2_s1_ratio_low_bpm'], p['s2_s1_ratio_high_bpm'])))
         boost_at = p.get('s1_s2_boost_ratio', 1.2)
         if r21 > r_max:
             pmin, pmax = p.get("penalty_amount_min", 0.15), p.get("penalty_amount_max", 0.40)
-            amt = pmin + np.clip((r21 / r_max - 1.0) / 2.0, 0, 1) * (pmax - pmin)
+            amt = pmin + _clip((r21 / r_max - 1.0) / 2.0, 0, 1) * (pmax - pmin)
             conf -= amt
             why += f"\n- PENALIZED by {amt:.2f} (S2 Str. Ratio {r21:.1f}x > Expected {r_max:.1f}x)"
         elif a1 > a2 * boost_at:
             bmin, bmax = p.get("boost_amount_min", 0.10), p.get("boost_amount_max", 0.35)
             r12 = a1 / (a2 + 1e-9)
-            amt = bmin + np.clip((r12 - boost_at) / (4.0 - boost_at), 0, 1) * (bmax - bmin)
+            amt = bmin + _clip((r12 - boost_at) / (4.0 - boost_at), 0, 1) * (bmax - bmin)
             conf += amt
             why += f"\n- BOOSTED by {amt:.2f} (S1 Str. Ratio {r12:.1f}x > S2)"
         conf = max(0.0, min(1.0, conf))
@@ -157,7 +198,7 @@ class PeakClassifier:
             z0 = cap * p.get("interval_penalty_start_factor", 1.0)
             z1 = cap * p.get("interval_penalty_full_factor", 1.4)
             if gap > z0:
-                amt = np.clip((gap - z0) / (z1 - z0 + 1e-9), 0, 1) * p.get("interval_max_penalty", 0.75)
+                amt = _clip((gap - z0) / (z1 - z0 + 1e-9), 0, 1) * p.get("interval_max_penalty", 0.75)
                 conf = max(0, conf - amt)
                 why += f"\n- Interval PENALTY by {amt:.2f} (Interval {gap:.3f}s > Max {cap:.3f}s)"
         thr = p['pairing_confidence_threshold']
@@ -165,16 +206,16 @@ class PeakClassifier:
         why += f"\n- Final Score: {conf:.2f} vs Threshold {thr:.2f} -> {'Paired' if ok else 'Not Paired'}"
         return ok, why
 
-    def _lone(self, j: int, last: int, ltb: float) -> Tuple[bool, str, bool]:
-        """Lone-S1 validation of raw peak #j after beat ``last`` (:304-329, :1201-1237).
+    def _lone(self, j: int, jl: int, ltb: float) -> Tuple[bool, str, bool]:
+        """Lone-S1 validation of raw peak #j after the beat at raw peak #jl (:304-329, :1201-1237).
         Returns (valid, detail, rejected_on_rhythm)."""
-        p, sr, env = self.params, self.sample_rate, self.audio_envelope
-        cur = self.peaks[j]
+        p, sr, env = self.params, self.sample_rate, self._envpk
+        cur, last = self._pkl[j], self._pkl[jl]
         exp_rr = 60.0 / ltb
         rr = (cur - last) / sr
-        rs = np.interp(abs(rr - exp_rr) / exp_rr, _RHYTHM_X, _RHYTHM_Y)
-        ar = self._strength(cur) / (self._strength(last) + 1e-9)
-        am = np.interp(ar, _AMP_X, _AMP_Y)
+        rs = _interp(abs(rr - exp_rr) / exp_rr, _RHYTHM_X, _RHYTHM_Y)
+        ar = self._str[j] / (self._str[jl] + 1e-9)
+        am = _interp(ar, _AMP_X, _AMP_Y)
         wr, wa = p.get('lone_s1_rhythm_weight', 0.65), p.get('lone_s1_amplitude_weight', 0.35)
         conf = (rs * wr) + (am * wa)
         why = (f"Rhythm Fit={rs:.2f} (Interval {rr:.3f}s vs Expected {exp_rr:.3f}s), "
@@ -182,10 +223,9 @@ class PeakClassifier:
         thr = p.get("lone_s1_confidence_threshold", 0.6)
         if conf < thr:
             return False, f"Rejected Lone S1: Confidence {conf:.2f} < Threshold {thr:.2f}. ({why})", True
-        if j < len(self.peaks) - 1:
-            nxt = self.peaks[j + 1]
-            fwd = (nxt - cur) / sr
-            if fwd < exp_rr * p.get('lone_s1_forward_check_pct', 0.6) and not (env[cur] > (env[nxt] * 1.7)):
+        if j < len(self._pkl) - 1:
+            fwd = (self._pkl[j + 1] - cur) / sr
+            if fwd < exp_rr * p.get('lone_s1_forward_check_pct', 0.6) and not (env[j] > (env[j + 1] * 1.7)):
                 implied = 60.0 / fwd if fwd > 0 else float('inf')
                 return False, f"Rejected Lone S1: Forward check failed (Implies {implied:.0f} BPM)", False
         return True, (f"Validated Lone S1: Confidence {conf:.3f} >= Threshold {thr:.2f}. ({why}, Weights: "
@@ -195,6 +235,7 @@ class PeakClassifier:
     def classify_peaks(self) -> Tuple[np.ndarray, np.ndarray, Dict]:
         """One left-to-right pass over the raw peaks (:113-221)."""
         pk, p, sr = self.peaks, self.params, self.sample_rate
+        pkl = self._pkl
         n = len(pk)
         if n < 2:
             return pk, pk, {"beat_debug_info": {}}
@@ -230,7 +271,7 @@ class PeakClassifier:
                 info[cur] = LONE_S1_LAST
                 j += 1
             else:
-                ok, why = self._pair(cur, pk[j + 1], ratio, ltb, len(beats))
+                ok, why = self._pair(j, ratio, ltb, len(beats))
                 if ok:
                     add_beat(j, True)
                     tag[j], tag[j + 1] = _T_S1, _T_S2
@@ -244,7 +285,7 @@ class PeakClassifier:
                     if not beats:
                         valid, detail, on_rhythm = True, "First beat", False
                     else:
-                        valid, detail, on_rhythm = self._lone(j, pk[beats[-1]], ltb)
+                        valid, detail, on_rhythm = self._lone(j, beats[-1], ltb)
                     if valid:
                         add_beat(j, False)
                         tag[j] = _T_LONE
@@ -266,7 +307,7 @@ class PeakClassifier:
                     j += 1
             # long-term BPM belief after every decision, from the last two beats (:203-212)
             if len(beats) > 1:
-                rr = (pk[beats[-1]] - pk[beats[-2]]) / sr
+                rr = (pkl[beats[-1]] - pkl[beats[-2]]) / sr
                 if rr > 0:
                     ltb = update_long_term_bpm(rr, ltb, p)
             if beats:
