@@ -653,9 +653,9 @@ def analyze_wav_file(wav_file_path: str, params: Dict, start_bpm_hint: Optional[
                      output_directory: str, mode: Optional[str] = None, device: int = 0):
     """The reference entry point (:1725) on the GPU path: preprocess + floor + raw
     peaks in one batched run, then the host stages above; writes the filtered
-    debug WAVs, ``<base>_bpm_plot.csv`` and the ReportGenerator files
-    (reports.py: summary, debug log, settings).  The interactive HTML plot
-    (Plotter's plotly figure) is not produced.  Returns None."""
+    debug WAVs, ``<base>_bpm_plot.html`` (plot.py), ``<base>_bpm_plot.csv``
+    and the ReportGenerator files (reports.py: summary, debug log, settings),
+    in the reference's order.  Returns None."""
     from .dropin import analyze_wav_files
     r = analyze_wav_files([wav_file_path], params, output_directory, mode=mode, device=device)[0]
     if "error" in r:
@@ -663,11 +663,15 @@ def analyze_wav_file(wav_file_path: str, params: Dict, start_bpm_hint: Optional[
     res = analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], r["peaks"], params, start_bpm_hint)
     m = res["final_metrics"]
     if m is not None:
+        from .plot import write_plot
         from .reports import write_reports
+        env = np.asarray(r["env"], dtype=np.float64)
+        write_plot(original_file_path, output_directory, params, r["sr"], env, res["all_raw_peaks"],
+                   res["analysis_data"], m)
         base = os.path.basename(os.path.splitext(original_file_path)[0])
         write_bpm_csv(os.path.join(output_directory, f"{base}_bpm_plot.csv"), m)
-        write_reports(original_file_path, output_directory, np.asarray(r["env"], dtype=np.float64), r["sr"],
-                      res["all_raw_peaks"], res["analysis_data"], m, start_bpm_hint)
+        write_reports(original_file_path, output_directory, env, r["sr"], res["all_raw_peaks"],
+                      res["analysis_data"], m, start_bpm_hint)
     return None
 
 

@@ -1,4 +1,4 @@
-"""Text reports of analyze_wav_file (the text half).
+"""Text reports of analyze_wav_file (the plot is plot.py).
 
 Restates the reference's ``ReportGenerator`` (bpm_analysis.py:782-985) and the
 two detail formatters it borrows from ``Plotter`` (:336-427):
@@ -8,8 +8,8 @@ two detail formatters it borrows from ``Plotter`` (:336-427):
 * ``<base>_Debug_Log.md``            one entry per labelled peak / trough :815-906
 
 Same bytes as the reference except the one "generated on" timestamp line of
-each markdown file (``now`` is injectable for tests).  The interactive HTML
-plot (``Plotter.plot_and_save``'s plotly figure) is not produced.
+each markdown file (``now`` is injectable for tests).  The interactive plot
+is plot.py.
 """
 from __future__ import annotations
 

@@ -8,7 +8,8 @@ two long synthetic recordings (regenerated bit-exactly by
 reference's stages 2-6 of ``analyze_wav_file`` (bpm_analysis.py:1734-1757):
 ``_run_preliminary_pass`` (:1623), ``PeakClassifier.classify_peaks`` (:113),
 ``_refine_and_correct_peaks`` (:1655), ``_calculate_final_metrics`` (:1701),
-the BPM CSV written by ``Plotter.plot_and_save`` (:458-473) and the
+the ``Plotter`` figure (its plotly JSON, :429-780), the BPM CSV it writes
+(:458-473) and the
 ``ReportGenerator`` files (summary, debug log, settings; :782-985).  It records
 the outputs as data in ``tests/golden/beats/<name>.npz``.
 
@@ -17,6 +18,7 @@ the outputs as data in ``tests/golden/beats/<name>.npz``.
 from __future__ import annotations
 
 import glob
+import hashlib
 import json
 import logging
 import os
@@ -102,7 +104,10 @@ def run_case(name, env, sr, floor, troughs, params, hint):
         out["hrv_" + c] = h[c].to_numpy(float) if len(h) else np.zeros(0)
     with tempfile.TemporaryDirectory() as td:
         p = R.Plotter(os.path.join(td, name + ".wav"), params, sr, td)
-        p.plot_and_save(env, raw, data, m)
+        fig_json = p.plot_and_save(env, raw, data, m).to_json()
+        out["fig_sha256"] = hashlib.sha256(fig_json.encode()).hexdigest()
+        if len(fig_json) < 600_000:
+            out["fig_json"] = fig_json
         csv_path = os.path.join(td, name + "_bpm_plot.csv")
         out["csv"] = open(csv_path).read() if os.path.exists(csv_path) else ""
         # ReportGenerator (:782-985); the one timestamp line of each markdown file is dropped

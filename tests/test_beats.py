@@ -173,3 +173,27 @@ def test_reports_match_reference(name, tmp_path):
     assert _drop_stamp(got("_Analysis_Summary.md")) == str(g["summary_md"])
     assert _drop_stamp(got("_Debug_Log.md")) == str(g["debug_log_md"])
     assert got("_Analysis_Settings.json") == str(g["settings_json"])
+
+
+@pytest.mark.parametrize("name", [c for c in CASES])
+def test_plot_matches_reference(name, tmp_path):
+    """The analysis figure's plotly JSON equals the reference Plotter's (hash for
+    every case; the JSON itself is kept for the small ones to show a diff)."""
+    import hashlib
+    from bpm_analysis_amd import plot as PL
+    g, params, hint, inp = load_case(name)
+    if "fig_sha256" not in g:
+        pytest.skip("the reference draws no figure for this case")
+    res = B.analyze_recording(inp["env"], inp["sr"], inp["floor"], inp["troughs"], inp["peaks"], params, hint)
+    fig = PL.write_plot(os.path.join(str(tmp_path), name + ".wav"), str(tmp_path), params, inp["sr"], inp["env"],
+                        res["all_raw_peaks"], res["analysis_data"], res["final_metrics"])
+    js = fig.to_json()
+    if "fig_json" in g:
+        want = json.loads(str(g["fig_json"]))
+        got = json.loads(js)
+        assert len(got["data"]) == len(want["data"])
+        for i, (a, b) in enumerate(zip(got["data"], want["data"])):
+            assert a == b, f"trace {i} ({b.get('name')})"
+        assert got["layout"] == want["layout"]
+    assert hashlib.sha256(js.encode()).hexdigest() == str(g["fig_sha256"])
+    assert (tmp_path / f"{name}_bpm_plot.html").stat().st_size > 0

@@ -431,6 +431,7 @@ def test_beat_stages_on_gpu_outputs(tmp_path):
         assert TB._drop_stamp((tmp_path / f"{name}_Analysis_Summary.md").read_text()) == str(g["summary_md"])
         assert TB._drop_stamp((tmp_path / f"{name}_Debug_Log.md").read_text()) == str(g["debug_log_md"])
         assert (tmp_path / f"{name}_Analysis_Settings.json").read_text() == str(g["settings_json"])
+        assert (tmp_path / f"{name}_bpm_plot.html").stat().st_size > 0
 
 
 def test_beat_stages_batch_of_hot_path_goldens():
