@@ -675,17 +675,31 @@ def analyze_wav_file(wav_file_path: str, params: Dict, start_bpm_hint: Optional[
     return None
 
 
-def analyze_many(results: Sequence[Dict], params: Dict, start_bpm_hint: Optional[float] = None) -> List[Dict]:
+def _analyze_one(job):
+    r, params, hint = job
+    if "error" in r:
+        return r
+    try:
+        return analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], r["peaks"], params, hint)
+    except Exception as exc:                      # per-file, as the GUI's loop catches it (gui.py:247-251)
+        return {"error": exc}
+
+
+def analyze_many(results: Sequence[Dict], params: Dict, start_bpm_hint: Optional[float] = None,
+                 workers: int = 1) -> List[Dict]:
     """``analyze_recording`` over the per-file dicts of a batched GPU run
-    (dropin.analyze_batch / analyze_wav_files); entries with ``error`` pass through."""
-    out = []
-    for r in results:
-        if "error" in r:
-            out.append(r)
-            continue
-        try:
-            out.append(analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], r["peaks"], params,
-                                         start_bpm_hint))
-        except Exception as exc:                  # per-file, as the GUI's loop catches it (gui.py:247-251)
-            out.append({"error": exc})
-    return out
+    (dropin.analyze_batch / analyze_wav_files); entries with ``error`` pass
+    through, and a file whose stages raise comes back as ``{"error": exc}``.
+
+    The stages are sequential per file but files are independent: with
+    ``workers > 1`` they run in that many CPU-only processes (spawned fresh, so
+    they never touch the GPU context of this one), ``chunksize`` files at a time."""
+    jobs = [({k: r[k] for k in ("env", "sr", "floor", "troughs", "peaks") if k in r} if "error" not in r else r,
+             params, start_bpm_hint) for r in results]
+    if workers <= 1 or len(jobs) < 2:
+        return [_analyze_one(j) for j in jobs]
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    chunk = max(1, len(jobs) // (4 * workers))
+    with ProcessPoolExecutor(max_workers=workers, mp_context=multiprocessing.get_context("spawn")) as ex:
+        return list(ex.map(_analyze_one, jobs, chunksize=chunk))

@@ -197,3 +197,22 @@ def test_plot_matches_reference(name, tmp_path):
         assert got["layout"] == want["layout"]
     assert hashlib.sha256(js.encode()).hexdigest() == str(g["fig_sha256"])
     assert (tmp_path / f"{name}_bpm_plot.html").stat().st_size > 0
+
+
+def test_analyze_many_worker_processes():
+    """The per-file stages over worker processes give what the sequential loop gives."""
+    names = ["ref_44k_60s_mono", "ref_44k_40s_clicks", "ref_44k_10s_zeros", "vulpine"]
+    runs, params = [], None
+    for n in names:
+        g, params, hint, inp = load_case(n)
+        runs.append(dict(inp))
+    seq = B.analyze_many(runs, params)
+    par = B.analyze_many(runs, params, workers=2)
+    for a, b in zip(seq, par):
+        assert ("error" in a) == ("error" in b)
+        if "error" in a:
+            assert type(a["error"]) is type(b["error"])
+            continue
+        assert np.array_equal(a["final_peaks"], b["final_peaks"])
+        assert a["analysis_data"]["beat_debug_info"] == b["analysis_data"]["beat_debug_info"]
+        pd.testing.assert_series_equal(a["final_metrics"]["smoothed_bpm"], b["final_metrics"]["smoothed_bpm"])
