@@ -203,11 +203,24 @@ class Detector:
     # ------------------------------------------------------------------ #
     def run_host(self, recordings: List[np.ndarray], fs: int, params: dict, mode: str = "reference",
                  stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False,
-                 options: int = 0) -> List[dict]:
-        """Host arrays in, per-file host results out (H2D + run + D2H)."""
+                 options: int = 0, longest_first: bool = True) -> List[dict]:
+        """Host arrays in, per-file host results out (H2D + run + D2H).
+
+        A ragged batch runs longest recording first (shard.longest_first: LPT
+        over the CUs, since recording f is workgroup f of every per-recording
+        kernel); results come back in the caller's order."""
         torch = _torch()
         if not recordings:
             return []
+        if longest_first and len({r.shape[0] for r in recordings}) > 1:
+            from .shard import longest_first as _lf
+            perm = _lf([r.shape[0] for r in recordings])
+            res = self.run_host([recordings[i] for i in perm], fs, params, mode=mode, stages=stages,
+                                want_y=want_y, log=log, options=options, longest_first=False)
+            out: List[dict] = [None] * len(recordings)
+            for k, i in enumerate(perm):
+                out[i] = res[k]
+            return out
         dt = recordings[0].dtype
         ch = 1 if recordings[0].ndim == 1 else recordings[0].shape[1]
         for r in recordings:

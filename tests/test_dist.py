@@ -67,3 +67,43 @@ def test_algorithmic_bytes_native_reads_pcm_once():
     ab = bench.algorithmic_bytes("native", 1024, 2646000, 18124, 146)
     assert ab["k_native_blocks"] == 1024 * 2646000 * 2
     assert set(ab) >= {"k_rollq_wm", "k_native_carry", "k_hilbert_env", "k_find_peaks[peaks]"}
+
+
+def _lpt_worker(rank, world, port, q):
+    """Every rank derives the same LPT placement from the lengths alone."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import numpy as np
+    from bpm_analysis_amd.shard import lpt_partition
+    rng = np.random.default_rng(5)
+    lengths = (rng.integers(10, 31, size=37) * 60 * 96000).tolist()     # C5-like: 10-30 min at 96 kHz
+    mine = lpt_partition(lengths, world)[rank]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    q.put((rank, got, lengths))
+    dist.destroy_process_group()
+
+
+def test_two_rank_lpt_placement():
+    import numpy as np
+    from bpm_analysis_amd.shard import longest_first, lpt_partition, makespan
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_lpt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, parts, lengths = outs[0]
+    assert all(o[1] == parts for o in outs)                     # ranks agree without exchanging a plan
+    flat = sorted(i for part in parts for i in part)
+    assert flat == list(range(len(lengths)))                    # each recording exactly once
+    n = np.asarray(lengths)
+    assert makespan(lengths, parts) <= n.sum() / world + n.max()   # greedy LPT bound
+    for part in parts:                                          # each rank's list is longest first
+        assert list(n[part]) == sorted(n[part], reverse=True)
+    assert list(longest_first([3, 5, 5, 1])) == [1, 2, 0, 3]     # stable among equal lengths
+    assert lpt_partition([7, 7, 7, 7], 2) == [[0, 2], [1, 3]]

@@ -445,3 +445,17 @@ def test_beat_stages_batch_of_hot_path_goldens():
         r = dropin.analyze_batch([h["pcm"]], int(h["fs"]), params, mode="reference")[0]
         assert np.array_equal(r["env"], inp["env"]) and np.array_equal(r["peaks"], inp["peaks"])
         TB.check_against_golden(g, B.analyze_many([r], params, hint)[0])
+
+
+def test_longest_first_order_is_transparent(det):
+    """run_host's longest-first dispatch order (shard.py) returns the caller's order, unchanged results."""
+    names = ["ref_44k_20s_wrap", "ref_44k_60s_mono", "ref_44k_short16", "ref_44k_40s_clicks"]
+    gs = [G.load(n) for n in names]
+    a = det.run_host([g["pcm"] for g in gs], 44100, G.BASE_PARAMS, mode="reference")
+    b = det.run_host([g["pcm"] for g in gs], 44100, G.BASE_PARAMS, mode="reference", longest_first=False)
+    for g, ra, rb in zip(gs, a, b):
+        for k in ("env", "floor", "troughs", "peaks"):
+            assert _same(ra[k], rb[k]), k
+        assert ra["flags"] == rb["flags"]
+        if not (ra["flags"] & 8):
+            _check_file(ra, g)
