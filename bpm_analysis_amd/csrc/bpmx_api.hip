@@ -417,15 +417,29 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
                        wm_full);
             }
             if (!need_merge) return BPMX_OK;
+            /* long recordings: a workgroup per chunk of outputs (each chunk pays
+             * one extra window fill: ~13 merge rounds against 32 or 16 tiles) */
+            int rq_rc = BPMX_OK;
+            int32_t *vfl = (int32_t *)ctx->buf("rollq_valid", (size_t)F * 8, &rq_rc);
+            if (rq_rc != BPMX_OK) return rq_rc;
+            a.vfirst = vfl;
+            a.vlast = vfl + F;
+            a.chunk = ((int64_t)F * ((maxnd + 8191) / 8192) >= 1024) ? 8192 : 4096;
+            const int64_t nch = (maxnd + a.chunk - 1) / a.chunk;
+            if (nch > 65535) return fail(BPMX_E_LIMIT, "recording too long for the chunked rolling quantile");
+            HIP_TRY(hipMemsetAsync(a.vfirst, 0x7F, (size_t)F * 4, s));      /* 0x7F7F7F7F: above any index */
+            HIP_TRY(hipMemsetAsync(a.vlast, 0xFF, (size_t)F * 4, s));       /* -1 */
+            const dim3 gq((unsigned)F, (unsigned)nch);
             if (cap <= 16 * RQ_T) {
                 (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 16>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 16>), dim3(F), dim3(RQ_T), lds, s, a);
+                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 16>), gq, dim3(RQ_T), lds, s, a);
             } else {
                 (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 32>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 32>), dim3(F), dim3(RQ_T), lds, s, a);
+                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 32>), gq, dim3(RQ_T), lds, s, a);
             }
+            LAUNCH(ctx, s, "k_rollq_fill", k_rollq_fill, dim3(4, (unsigned)F), dim3(256), 0, s, a);
             return BPMX_OK;
         };
         const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, 8), F);

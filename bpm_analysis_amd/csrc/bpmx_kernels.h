@@ -97,6 +97,8 @@ struct RollqArgs {
     int32_t wm_max;          /* k_rolling_quantile skips files with n <= wm_max (k_rollq_wm took them) */
     const double *env;       /* k_rollq_wm: interpolate dense from env at the troughs itself ... */
     const int32_t *ntr;      /* ... when the file has <= WM_TRMAX of them (else read dense) */
+    int64_t chunk;           /* k_rolling_quantile: outputs per workgroup (blockIdx.y = chunk of the file) */
+    int32_t *vfirst, *vlast; /* [F] first / last valid output over all chunks (k_rollq_fill reads them) */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -171,6 +173,7 @@ __global__ void k_draft_bounds(DraftBoundArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);
+__global__ void k_rollq_fill(RollqArgs A);
 
 /* wavelet-matrix rolling quantile (k_rollq_wm.hip): one 1024-thread workgroup
  * per recording of <= WM_MMAX decimated samples */

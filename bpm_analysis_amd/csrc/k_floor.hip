@@ -63,6 +63,10 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
     if (A.doff[f + 1] - A.doff[f] <= A.wm_max) return;       /* done by k_rollq_wm */
+    /* chunk blockIdx.y of the outputs: the window is local, so a chunk starts
+     * from an empty union and fills it from its own first window */
+    const int64_t c0 = (int64_t)blockIdx.y * A.chunk;
+    if (c0 >= A.doff[f + 1] - A.doff[f]) return;
     extern __shared__ __align__(16) unsigned char smem[];
     const int cap = A.cap;
     /* LDS carve-up (rollq_lds_bytes); single sorted buffer A: a merge reads the
@@ -85,6 +89,7 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     double *out = A.out + d0;
     const int64_t W = A.window, minp = A.min_periods;
     const int64_t t0 = A.troughs[d0];
+    const int64_t cend = c0 + A.chunk < n ? c0 + A.chunk : n;
     const double q = A.q;
     const double INF = __builtin_inf();
     if (tid == 0) { s_first = INT_MAX; s_last = -1; }
@@ -95,8 +100,8 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     /* the next tile's first chunk of new samples is loaded during this tile's walk */
     double vpre = INF;
     int64_t apre = -1;
-    for (int64_t i0 = 0; i0 < n; i0 += T) {
-        const int64_t i1 = i0 + T < n ? i0 + T : n;
+    for (int64_t i0 = c0; i0 < cend; i0 += T) {
+        const int64_t i1 = i0 + T < cend ? i0 + T : cend;
         int64_t sA, eA, sB, eB;
         win_bounds(i0, n, W, sA, eA);
         win_bounds(i1 - 1, n, W, sB, eB);
@@ -212,8 +217,8 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
         } while (a < P1);
         P0prev = P0;
         P1prev = P1 > P1prev ? P1 : P1prev;
-        if (i0 + T < n) {   /* prefetch the next tile's first chunk of new samples */
-            const int64_t i0n = i0 + T, i1n = i0n + T < n ? i0n + T : n;
+        if (i0 + T < cend) {   /* prefetch the next tile's first chunk of new samples */
+            const int64_t i0n = i0 + T, i1n = i0n + T < cend ? i0n + T : cend;
             int64_t sAn, eAn, sBn, eBn;
             win_bounds(i0n, n, W, sAn, eAn);
             win_bounds(i1n - 1, n, W, sBn, eBn);
@@ -326,16 +331,32 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
         STAMP(5);
     }
     STAMP_FLUSH(A.stamps);
-    /* ---- .bfill().ffill() ---- */
-    const int first = s_first, last = s_last;
+    /* first / last valid output of this chunk -> the recording's (k_rollq_fill) */
+    if (tid == 0 && s_last >= 0) {
+        atomicMin(&A.vfirst[f], s_first);
+        atomicMax(&A.vlast[f], s_last);
+    }
+}
+
+/* .bfill().ffill() of the chunked rolling quantile: nobs(i) is unimodal, so
+ * the NaN outputs are a prefix and a suffix; fill them from the first and
+ * last valid output over all chunks (or flag the recording all-NaN). */
+__global__ __launch_bounds__(256) void k_rollq_fill(RollqArgs A) {
+    const int f = blockIdx.y;
+    if (f >= A.n_files || !A.run[f]) return;
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    if (n <= A.wm_max) return;
+    const int first = A.vfirst[f], last = A.vlast[f];
     if (last < 0) {
-        if (tid == 0) A.allnan[f] = 1;
+        if (blockIdx.x == 0 && threadIdx.x == 0) A.allnan[f] = 1;
         return;
     }
-    if (tid == 0) A.allnan[f] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.allnan[f] = 0;
+    double *out = A.out + d0;
     const double vf = out[first], vl = out[last];
-    for (int64_t i = tid; i < first; i += T) out[i] = vf;
-    for (int64_t i = last + 1 + tid; i < n; i += T) out[i] = vl;
+    const int64_t stride = (int64_t)gridDim.x * 256, i00 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (int64_t i = i00; i < first; i += stride) out[i] = vf;
+    for (int64_t i = last + 1 + i00; i < n; i += stride) out[i] = vl;
 }
 
 template __global__ void k_rolling_quantile<256, 16>(RollqArgs A);

@@ -65,11 +65,16 @@ int main(int argc, char **argv) {
         a.dense = d_dense; a.doff = d_doff; a.troughs = d_tr; a.run = d_run; a.n_files = F; a.window = W;
         a.min_periods = 3; a.cap = cap; a.q = 0.2; a.out = d_out; a.allnan = d_an; a.stamps = d_st;
         a.wm_max = 0; a.env = nullptr; a.ntr = nullptr;
+        a.chunk = (int64_t)1 << 40;                    /* one chunk per recording (the fill pass is not timed) */
+        CK(hipMalloc(&a.vfirst, F * 8));
+        a.vlast = a.vfirst + F;
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         float best = 1e9;
         for (int rep = 0; rep < 4; ++rep) {
+            CK(hipMemset(a.vfirst, 0x7F, F * 4));
+            CK(hipMemset(a.vlast, 0xFF, F * 4));
             CK(hipEventRecord(e0, 0));
             if (cap <= 16 * 256) {
                 CK(hipFuncSetAttribute((const void *)k_rolling_quantile<256, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--fs", type=int, default=44100)
     ap.add_argument("--mode", default="native")
+    ap.add_argument("--min-s", type=int, default=60)
+    ap.add_argument("--max-s", type=int, default=600)
     args = ap.parse_args()
     import torch
     from bpm_analysis_amd import DEFAULT_PARAMS
@@ -30,7 +32,7 @@ def main():
     params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
     fs = args.fs
     rng = np.random.default_rng(3)
-    lens = (rng.integers(60, 601, size=args.files) * fs).astype(np.int64)      # 1-10 min
+    lens = (rng.integers(args.min_s, args.max_s + 1, size=args.files) * fs).astype(np.int64)
     d = design(fs, params, log=False)
     det = Detector(0)
     out = {}
@@ -47,8 +49,13 @@ def main():
             det.run(pcm, fo, fs, params, mode=args.mode, out=res, d=d)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
+        det.profile(True)
+        det.run(pcm, fo, fs, params, mode=args.mode, out=res, d=d)
+        torch.cuda.synchronize()
+        det.profile(False)
+        kern = {k: round(v[1], 3) for k, v in sorted(det.profile_read().items(), key=lambda kv: -kv[1][1])}
         out[name] = {"ms_per_step": dt * 1e3, "audio_samples_per_s": float(lens.sum()) / dt,
-                     "peaks": int(res.n_peaks.sum())}
+                     "peaks": int(res.n_peaks.sum()), "kernel_ms": kern}
         del pcm, res
         torch.cuda.empty_cache()
     out.update(files=args.files, total_samples=int(lens.sum()), fs=fs, mode=args.mode,
