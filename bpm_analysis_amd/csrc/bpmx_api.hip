@@ -111,6 +111,11 @@ void bpmx_destroy(bpmx_ctx *ctx) {
         if (kv.second.first) (void)hipFree(kv.second.first);
     for (auto &r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : ctx->pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < bpmx_ctx::NSIDE; ++i) {
+        if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
+        if (ctx->side_join[i]) (void)hipEventDestroy(ctx->side_join[i]);
+    }
+    if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
     delete ctx;
 }
 

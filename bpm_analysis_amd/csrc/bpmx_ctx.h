@@ -42,6 +42,20 @@ struct bpmx_ctx {
     std::vector<hipEvent_t> pool;
     std::string prof_only;              /* bpmx_profile_only: record this label only (empty: all) */
     std::map<std::string, std::pair<long, double>> totals;
+    /* side streams for the native-mode rocFFT runs (one plan per distinct Nd:
+     * small, latency-bound executions that overlap when spread out) */
+    static constexpr int NSIDE = 4;
+    hipStream_t side[NSIDE] = {};
+    hipEvent_t side_fork = nullptr, side_join[NSIDE] = {};
+    bool side_ready() {
+        if (side[0]) return true;
+        for (int i = 0; i < NSIDE; ++i) {
+            if (hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&side_join[i], hipEventDisableTiming) != hipSuccess)
+                return false;
+        }
+        return hipEventCreateWithFlags(&side_fork, hipEventDisableTiming) == hipSuccess;
+    }
 
     /* grow-only device scratch; *grew (optional) reports a fresh allocation,
      * whose contents the caller must re-upload */

@@ -1391,6 +1391,8 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     bool need_env = false;
     std::vector<int32_t> &fused = ctx->nat_fused;
     fused.assign(F, 0);
+    bool side_used[bpmx_ctx::NSIDE] = {};
+    bool forked = false;
     int f0 = 0;
     while (f0 < F) {
         const int64_t nd = doff[f0 + 1] - doff[f0];
@@ -1422,24 +1424,37 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             need_env = true;
             FftPlans *pl = nullptr;
             if ((rc = get_plans(ctx->device, nd, f1 - f0, &pl)) != BPMX_OK) return rc;
-            void *work = pl->work ? ctx->buf("nat_fft_work", pl->work, &rc) : nullptr;
+            /* each run on a side stream chosen by Nd (a plan never runs on two
+             * streams at once), its own work buffer; joined back into s below */
+            if (!forked) {
+                if (!ctx->side_ready()) return fail(BPMX_E_HIP, "side stream creation failed");
+                HIP_TRY(hipEventRecord(ctx->side_fork, s));
+                forked = true;
+            }
+            const int si = (int)(nd % bpmx_ctx::NSIDE);
+            hipStream_t ss = ctx->side[si];
+            if (!side_used[si]) {
+                HIP_TRY(hipStreamWaitEvent(ss, ctx->side_fork, 0));
+                side_used[si] = true;
+            }
+            void *work = pl->work ? ctx->buf("nat_fft_work" + std::to_string(si), pl->work, &rc) : nullptr;
             if (rc != BPMX_OK) return rc;
             rocfft_execution_info info = nullptr;
             rocfft_execution_info_create(&info);
-            rocfft_execution_info_set_stream(info, s);
+            rocfft_execution_info_set_stream(info, ss);
             if (work) rocfft_execution_info_set_work_buffer(info, work, pl->work);
             void *in[1] = {yd + doff[f0]};
             void *out[1] = {z + doff[f0]};
             {
-                Launch l(ctx, s, "rocfft_r2c");
+                Launch l(ctx, ss, "rocfft_r2c");
                 rocfft_status st = rocfft_execute(pl->fwd, in, out, info);
                 if (st != rocfft_status_success) { rocfft_execution_info_destroy(info); return fft_fail("rocfft_execute(r2c)", st); }
                 if ((rc = l.done()) != BPMX_OK) { rocfft_execution_info_destroy(info); return rc; }
             }
-            LAUNCH(ctx, s, "k_hilbert_rotate", k_hilbert_rotate, dim3((unsigned)((nd / 2 + 256) / 256), f1 - f0),
-                   dim3(256), 0, s, z, d_doff, d_active, f0, f1);
+            LAUNCH(ctx, ss, "k_hilbert_rotate", k_hilbert_rotate, dim3((unsigned)((nd / 2 + 256) / 256), f1 - f0),
+                   dim3(256), 0, ss, z, d_doff, d_active, f0, f1);
             {
-                Launch l(ctx, s, "rocfft_c2r");
+                Launch l(ctx, ss, "rocfft_c2r");
                 void *hout[1] = {hb + doff[f0]};
                 rocfft_status st = rocfft_execute(pl->inv, out, hout, info);
                 if (st != rocfft_status_success) { rocfft_execution_info_destroy(info); return fft_fail("rocfft_execute(c2r)", st); }
@@ -1449,6 +1464,11 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         }
         f0 = f1;
     }
+    for (int i = 0; i < bpmx_ctx::NSIDE; ++i)       /* join the side streams back into s */
+        if (side_used[i]) {
+            HIP_TRY(hipEventRecord(ctx->side_join[i], ctx->side[i]));
+            HIP_TRY(hipStreamWaitEvent(s, ctx->side_join[i], 0));
+        }
     if (need_env) {                                   /* the rocFFT runs (fused runs are skipped) */
         int32_t *d_fused = (int32_t *)ctx->buf("nat_fused", (size_t)F * 4, &rc);
         if (rc != BPMX_OK) return rc;
