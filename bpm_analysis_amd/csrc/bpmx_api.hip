@@ -475,7 +475,8 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.env = O->env; a.doff = d_doff; a.raw = rawt; a.nraw = d_nraw; a.run = d_run1; a.n_files = F;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
             a.dec = tdec; a.exact = d_exact;
-            LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F), dim3(DB_T), 0, s, a);
+            a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
+            LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, DB_TRMAX / DB_T), dim3(DB_T), 0, s, a);
         }
         if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {

@@ -136,9 +136,11 @@ struct DraftBoundArgs {
     double q, mult;
     uint8_t *dec;            /* [doff + j]: 1 keep, 0 reject, 2 undecided */
     int32_t *exact;          /* [F] out: 1 = needs the full draft (undecided trough, all-NaN draft, too many troughs) */
+    int32_t local_m;         /* more troughs than this: rank segments per window (DB_LOCAL_M) */
 };
 constexpr int DB_T = 256;
 constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */
+constexpr int DB_LOCAL_M = 512;  /* more troughs than this: per-window ranking instead of the global order */
 
 struct FinalArgs {
     const double *draft;

@@ -432,6 +432,14 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         if (tid == 0) A.exact[f] = 1;
         return;
     }
+    /* Long recordings (> local_m troughs) rank each window's segments in
+     * place, so their troughs split over blockIdx.y chunks of DB_T; shorter
+     * ones build the recording-wide order once, in chunk 0. */
+    const bool local = m > A.local_m;
+    if (!local && blockIdx.y > 0) return;
+    const int jc0 = local ? (int)blockIdx.y * DB_T : 0;
+    const int jc1 = local ? (jc0 + DB_T < m ? jc0 + DB_T : m) : m;
+    if (jc0 >= jc1) return;
     const int64_t *raw = A.raw + d0;
     const double *env = A.env + d0;
     if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; }
@@ -443,8 +451,10 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int64_t W = A.window, t0 = s_tp[0];
     auto seg_lo = [&](int j) -> double { return j + 1 < m ? fmin(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
     auto seg_hi = [&](int j) -> double { return j + 1 < m ? fmax(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
-    /* stable ranks by end value (ties by index): order lists for the walks */
-    for (int j = tid; j < m; j += DB_T) {
+    /* stable ranks by end value (ties by index): order lists for the walks.
+     * Long recordings skip them (O(m^2)) and rank each window's few segments
+     * in place instead (below). */
+    for (int j = tid; j < m && !local; j += DB_T) {
         const double a = seg_lo(j), b = seg_hi(j);
         int ra = 0, rb = 0;
         for (int i = 0; i < m; ++i) {
@@ -479,7 +489,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         return lo - 1;
     };
     bool any_undecided = false;
-    for (int j = tid; j < m; j += DB_T) {
+    for (int j = jc0 + tid; j < jc1; j += DB_T) {
         const int64_t t = s_tp[j];
         const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
         int64_t s, e;
@@ -498,19 +508,39 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         /* L: first lower end (ascending) whose in-window cumulative length exceeds k;
          * U: first upper end (ascending) whose cumulative reaches thr_u */
         double L = __builtin_inf(), U = __builtin_inf();
-        int64_t c = 0;
-        for (int r = 0; r < m; ++r) {
-            const int b = s_olo[r];
-            if (b < jl || b > jh) continue;
-            c += len_of(b);
-            if (c > k) { L = seg_lo(b); break; }
-        }
-        c = 0;
-        for (int r = 0; r < m; ++r) {
-            const int b = s_ohi[r];
-            if (b < jl || b > jh) continue;
-            c += len_of(b);
-            if (c >= thr_u) { U = seg_hi(b); break; }
+        if (!local) {
+            int64_t c = 0;
+            for (int r = 0; r < m; ++r) {
+                const int b = s_olo[r];
+                if (b < jl || b > jh) continue;
+                c += len_of(b);
+                if (c > k) { L = seg_lo(b); break; }
+            }
+            c = 0;
+            for (int r = 0; r < m; ++r) {
+                const int b = s_ohi[r];
+                if (b < jl || b > jh) continue;
+                c += len_of(b);
+                if (c >= thr_u) { U = seg_hi(b); break; }
+            }
+        } else {
+            /* the same walks without the global order: segment b's cumulative
+             * length over the window's segments ordered (value, index) <= b's;
+             * cumulative lengths never decrease along that order, so the
+             * walk's stopping segment has the least value among those whose
+             * cumulative length passes the threshold */
+            for (int b = jl; b <= jh; ++b) {
+                const double lb = seg_lo(b), hb = seg_hi(b);
+                int64_t cl = 0, ch = 0;
+                for (int i = jl; i <= jh; ++i) {
+                    const int64_t li = len_of(i);
+                    const double loi = seg_lo(i), hii = seg_hi(i);
+                    cl += (loi < lb || (loi == lb && i <= b)) ? li : 0;
+                    ch += (hii < hb || (hii == hb && i <= b)) ? li : 0;
+                }
+                if (cl > k) L = fmin(L, lb);
+                if (ch >= thr_u) U = fmin(U, hb);
+            }
         }
         const double et = s_tv[j];
         uint8_t dcs;
@@ -521,7 +551,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     }
     if (any_undecided) s_undecided = 1;
     __syncthreads();
-    if (tid == 0) A.exact[f] = s_undecided;
+    if (tid == 0 && s_undecided) A.exact[f] = 1;         /* zeroed before the launch */
 }
 
 __global__ __launch_bounds__(256) void k_floor_final(FinalArgs A) {

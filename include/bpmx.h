@@ -78,8 +78,10 @@ enum bpmx_option {
                                     (test/diagnostic; recordings the fused kernel cannot plan always use it) */
     BPMX_OPT_DRAFT_FULL = 8,     /* compute the draft floor (first rolling quantile) in full for every recording
                                     instead of deciding troughs from its bounds first (test/diagnostic) */
-    BPMX_OPT_ROLLQ_NOPRUNE = 16  /* wavelet-matrix rolling quantile over every sample, without first dropping
+    BPMX_OPT_ROLLQ_NOPRUNE = 16, /* wavelet-matrix rolling quantile over every sample, without first dropping
                                     the samples no window's quantile can reach (test/diagnostic) */
+    BPMX_OPT_DRAFT_GLOBAL_RANK = 32 /* draft-floor bounds from the recording-wide segment order even for
+                                       recordings of > 512 troughs (test/diagnostic; default ranks per window) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

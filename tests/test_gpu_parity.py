@@ -459,3 +459,26 @@ def test_longest_first_order_is_transparent(det):
         assert ra["flags"] == rb["flags"]
         if not (ra["flags"] & 8):
             _check_file(ra, g)
+
+
+@pytest.mark.parametrize("secs", [0, 420])
+def test_draft_bounds_window_ranking(det, secs):
+    """k_draft_bounds ranks each window's segments in place for recordings of
+    > 512 troughs; the recording-wide order (BPMX_OPT_DRAFT_GLOBAL_RANK) and the
+    full draft give the same floor, troughs and peaks (vulpine: 1456 raw
+    troughs; a 7-min recording: ~1700), and the oracle agrees."""
+    from bpm_analysis_amd import _native as N
+    if secs == 0:
+        g = G.load("vulpine")
+        env, sr, params = g["env"], int(g["sr"]), g["params"]
+        want = g
+    else:
+        pcm = O.synth(123, 44100 * secs, 44100, 1)
+        o = O.detect(pcm, 44100, G.BASE_PARAMS, mode="reference")
+        env, sr, params, want = o["env"], o["sr"], G.BASE_PARAMS, o
+    runs = [det.run_env_host([env], sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS, options=opt)[0]
+            for opt in (0, N.OPT_DRAFT_GLOBAL_RANK, N.OPT_DRAFT_FULL)]
+    for r in runs:
+        assert _same(r["floor"], want["floor"])
+        assert _same(r["troughs"], want["troughs"])
+        assert _same(r["peaks"], want["peaks"])
