@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbpmx.so")
+# BPMX_LIB: another build of the same library (diagnostic A/B runs of kernel variants)
+LIB_PATH = os.environ.get("BPMX_LIB") or os.path.join(_HERE, "libbpmx.so")
 
 ABI_VERSION = 1
 
