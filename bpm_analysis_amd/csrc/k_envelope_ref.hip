@@ -56,11 +56,15 @@ struct Df2t {
     double z0, z1, z2, z3;
     /* scipy DOUBLE filt loop: y = Z0 + b0*x; Z_k = Z_{k+1} + x*b_{k+1} - y*a_{k+1} */
     __device__ __forceinline__ double step(double xn) {
-        double yn = z0 + b0 * xn;
-        z0 = z1 + xn * b1 - yn * a1;
-        z1 = z2 + xn * b2 - yn * a2;
-        z2 = z3 + xn * b3 - yn * a3;
-        z3 = xn * b4 - yn * a4;
+        /* the same rounded operations, the x-only ones first: only
+         * z0 + b0 x -> y a1 -> (z1 + x b1) - y a1 is on the chain to the next y */
+        const double bx0 = b0 * xn, bx1 = xn * b1, bx2 = xn * b2, bx3 = xn * b3, bx4 = xn * b4;
+        const double p1 = z1 + bx1, p2 = z2 + bx2, p3 = z3 + bx3;
+        const double yn = z0 + bx0;
+        z0 = p1 - yn * a1;
+        z1 = p2 - yn * a2;
+        z2 = p3 - yn * a3;
+        z3 = bx4 - yn * a4;
         return yn;
     }
     __device__ __forceinline__ void init(const double *zi, double x0) {
@@ -91,6 +95,31 @@ struct RollMean {
             sum = t;
             if (__signbit(v)) neg--;
         }
+    }
+    /* branch-free forms (selects instead of the NaN / tie branches), the same
+     * rounded operations when they apply: one basic block per prefetch block */
+    __device__ __forceinline__ void add_sel(double v) {
+        const bool ok = v == v;
+        const double y = v - cadd, t = sum + y;
+        cadd = ok ? (t - sum) - y : cadd;
+        sum = ok ? t : sum;
+        nobs += ok ? 1 : 0;
+        neg += (ok && __signbit(v)) ? 1 : 0;
+        same = ok ? (v == prev ? same + 1 : 1) : same;
+        prev = ok ? v : prev;
+    }
+    __device__ __forceinline__ void remove_sel(double v) {
+        const bool ok = v == v;
+        const double y = -v - crem, t = sum + y;
+        crem = ok ? (t - sum) - y : crem;
+        sum = ok ? t : sum;
+        nobs -= ok ? 1 : 0;
+        neg -= (ok && __signbit(v)) ? 1 : 0;
+    }
+    __device__ __forceinline__ double mean_sel() const {
+        double r = sum / (double)nobs;
+        r = same >= nobs ? prev : ((neg == 0 && r < 0) || (neg == nobs && r > 0) ? 0.0 : r);
+        return nobs >= 1 ? r : __builtin_nan("");
     }
     __device__ __forceinline__ double mean() const {
         if (nobs >= 1) {
@@ -141,6 +170,12 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     int64_t ndmax = nd;
     for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmax, o); ndmax = t > ndmax ? t : ndmax; }
     if (ndmax == 0) return;
+    /* shortest running file of the wave: blocks below it need no per-step
+     * predicate, so a block's steps form one basic block the scheduler can
+     * interleave (the x-only products of later steps fill the latency of the
+     * y-dependent chain) */
+    int64_t ndmin = run ? nd : INT64_MAX;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmin, o); ndmin = t < ndmin ? t : ndmin; }
 
     Df2t D;
     D.b0 = A.b[0]; D.b1 = A.b[1]; D.b2 = A.b[2]; D.b3 = A.b[3]; D.b4 = A.b[4];
@@ -169,7 +204,12 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         for (int64_t j0 = 0; j0 < ndmax; j0 += PF) {
 #pragma unroll
             for (int u = 0; u < PF; ++u) nxt[u] = xd(j0 + PF + u);
-            if (run) {
+            if (j0 + PF <= ndmin) {
+                if (run) {
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) scr[(15 + j0 + u) * S] = D.step(cur[u]);
+                }
+            } else if (run) {
 #pragma unroll
                 for (int u = 0; u < PF; ++u)
                     if (j0 + u < nd) scr[(15 + j0 + u) * S] = D.step(cur[u]);
@@ -199,7 +239,12 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         for (int64_t r0 = 0; r0 < nemax; r0 += PF) {
 #pragma unroll
             for (int u = 0; u < PF; ++u) nxt[u] = ld(r0 + PF + u);
-            if (run) {
+            if (r0 + PF <= ndmin + 30) {
+                if (run) {
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
+                }
+            } else if (run) {
 #pragma unroll
                 for (int u = 0; u < PF; ++u)
                     if (r0 + u < ne) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
@@ -240,6 +285,17 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                 nr[u] = ldy(i + off - w);
                 if (yout) ny[u] = y[(i < last ? i : last) * S];
             }
+            if (w > 1 && i0 >= w - off && i0 + PF + off <= ndmin) {
+                /* every running lane removes and adds one sample per step here
+                 * (lanes that do not run compute values nobody stores) */
+#pragma unroll
+                for (int u = 0; u < PF; ++u) {
+                    R.remove_sel(cr[u]);
+                    R.add_sel(ca[u]);
+                    st_env[(i0 + u) & (STG - 1)][lane] = R.mean_sel();
+                    if (yout) st_y[(i0 + u) & (STG - 1)][lane] = cy[u];
+                }
+            } else
 #pragma unroll
             for (int u = 0; u < PF; ++u) {
                 const int64_t i = i0 + u;
