@@ -133,7 +133,11 @@ struct RollMean {
     }
 };
 
-constexpr int PF = 16;   /* prefetch block (steps) */
+#ifndef BPMX_REF_PFB
+#define BPMX_REF_PFB 16
+#endif
+constexpr int PF = 16;   /* prefetch block (steps), rolling-mean phase */
+constexpr int PFB = BPMX_REF_PFB;   /* prefetch block of the two filter passes */
 constexpr int STG = 64;  /* LDS staging rows */
 
 /* write the staged rows [base, base+rows) of every file in the wave, 512 B per store */
@@ -192,30 +196,30 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         const double x0 = xd(0), xl = xd(last);
 #pragma unroll
         for (int k = 0; k < 15; ++k) { padv[k] = xd(15 - k); padr[k] = xd(last - 1 - k); }
-        double cur[PF], nxt[PF];
+        double cur[PFB], nxt[PFB];
 #pragma unroll
-        for (int u = 0; u < PF; ++u) cur[u] = xd(u);
+        for (int u = 0; u < PFB; ++u) cur[u] = xd(u);
         if (run) {
             const double e0 = odd_ext(wdt, x0, padv[0]);
             D.init(A.zi, e0);
 #pragma unroll
             for (int k = 0; k < 15; ++k) scr[k * S] = D.step(odd_ext(wdt, x0, padv[k]));
         }
-        for (int64_t j0 = 0; j0 < ndmax; j0 += PF) {
+        for (int64_t j0 = 0; j0 < ndmax; j0 += PFB) {
 #pragma unroll
-            for (int u = 0; u < PF; ++u) nxt[u] = xd(j0 + PF + u);
-            if (j0 + PF <= ndmin) {
+            for (int u = 0; u < PFB; ++u) nxt[u] = xd(j0 + PFB + u);
+            if (j0 + PFB <= ndmin) {
                 if (run) {
 #pragma unroll
-                    for (int u = 0; u < PF; ++u) scr[(15 + j0 + u) * S] = D.step(cur[u]);
+                    for (int u = 0; u < PFB; ++u) scr[(15 + j0 + u) * S] = D.step(cur[u]);
                 }
             } else if (run) {
 #pragma unroll
-                for (int u = 0; u < PF; ++u)
+                for (int u = 0; u < PFB; ++u)
                     if (j0 + u < nd) scr[(15 + j0 + u) * S] = D.step(cur[u]);
             }
 #pragma unroll
-            for (int u = 0; u < PF; ++u) cur[u] = nxt[u];
+            for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
         }
         if (run) {
 #pragma unroll
@@ -232,25 +236,25 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
             row = row < 0 ? 0 : row;
             return scr[row * S];
         };
-        double cur[PF], nxt[PF];
+        double cur[PFB], nxt[PFB];
 #pragma unroll
-        for (int u = 0; u < PF; ++u) cur[u] = ld(u);
+        for (int u = 0; u < PFB; ++u) cur[u] = ld(u);
         if (run) D.init(A.zi, cur[0]);
-        for (int64_t r0 = 0; r0 < nemax; r0 += PF) {
+        for (int64_t r0 = 0; r0 < nemax; r0 += PFB) {
 #pragma unroll
-            for (int u = 0; u < PF; ++u) nxt[u] = ld(r0 + PF + u);
-            if (r0 + PF <= ndmin + 30) {
+            for (int u = 0; u < PFB; ++u) nxt[u] = ld(r0 + PFB + u);
+            if (r0 + PFB <= ndmin + 30) {
                 if (run) {
 #pragma unroll
-                    for (int u = 0; u < PF; ++u) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
+                    for (int u = 0; u < PFB; ++u) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
                 }
             } else if (run) {
 #pragma unroll
-                for (int u = 0; u < PF; ++u)
+                for (int u = 0; u < PFB; ++u)
                     if (r0 + u < ne) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
             }
 #pragma unroll
-            for (int u = 0; u < PF; ++u) cur[u] = nxt[u];
+            for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
         }
     }
     /* ---------------- |y| centred rolling mean over rows [15, 15+nd) ---------------- */
