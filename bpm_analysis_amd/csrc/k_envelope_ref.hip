@@ -75,7 +75,7 @@ struct Df2t {
 /* pandas roll_mean state (aggregations.pyx add_mean / remove_mean / calc_mean) */
 struct RollMean {
     double sum = 0, cadd = 0, crem = 0, prev = 0;
-    int64_t nobs = 0, neg = 0, same = 0;
+    int32_t nobs = 0, neg = 0, same = 0;   /* <= recording length (< 2^31, host-checked) */
     __device__ __forceinline__ void add(double v) {
         if (v == v) {
             nobs++;
@@ -105,7 +105,9 @@ struct RollMean {
         sum = ok ? t : sum;
         nobs += ok ? 1 : 0;
         neg += (ok && __signbit(v)) ? 1 : 0;
-        same = ok ? (v == prev ? same + 1 : 1) : same;
+        int32_t sn = v == prev ? same + 1 : 1;
+        __asm__ volatile("" : "+v"(sn));          /* keep it a select, not a branch */
+        same = ok ? sn : same;
         prev = ok ? v : prev;
     }
     __device__ __forceinline__ void remove_sel(double v) {
@@ -118,6 +120,7 @@ struct RollMean {
     }
     __device__ __forceinline__ double mean_sel() const {
         double r = sum / (double)nobs;
+        __asm__ volatile("" : "+v"(r));           /* divide every step (its latency overlaps), no branch */
         r = same >= nobs ? prev : ((neg == 0 && r < 0) || (neg == nobs && r > 0) ? 0.0 : r);
         return nobs >= 1 ? r : __builtin_nan("");
     }
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                     R.remove_sel(cr[u]);
                     R.add_sel(ca[u]);
                     st_env[(i0 + u) & (STG - 1)][lane] = R.mean_sel();
-                    if (yout) st_y[(i0 + u) & (STG - 1)][lane] = cy[u];
+                    st_y[(i0 + u) & (STG - 1)][lane] = cy[u];      /* flushed only when yout */
                 }
             } else
 #pragma unroll
