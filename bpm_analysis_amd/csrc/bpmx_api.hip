@@ -429,7 +429,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             if (rq_rc != BPMX_OK) return rq_rc;
             a.vfirst = vfl;
             a.vlast = vfl + F;
-            a.chunk = ((int64_t)F * ((maxnd + 8191) / 8192) >= 1024) ? 8192 : 4096;
+            /* 8192 outputs per chunk, halved (down to 1024) while the batch
+             * gives fewer than 1024 workgroups: a chunk's first-window fill is
+             * fixed overhead, worth paying only when CUs would sit idle */
+            a.chunk = 8192;
+            while (a.chunk > 1024 && (int64_t)F * ((maxnd + a.chunk - 1) / a.chunk) < 1024) a.chunk >>= 1;
             const int64_t nch = (maxnd + a.chunk - 1) / a.chunk;
             if (nch > 65535) return fail(BPMX_E_LIMIT, "recording too long for the chunked rolling quantile");
             HIP_TRY(hipMemsetAsync(a.vfirst, 0x7F, (size_t)F * 4, s));      /* 0x7F7F7F7F: above any index */
