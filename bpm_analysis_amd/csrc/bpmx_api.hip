@@ -332,7 +332,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
     const bool long_files = maxnd > QR_MAX;
     bool noise_lazy = false;
-    if (long_files) LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F), dim3(256), 0, s, bs);
+    if (long_files) {
+        /* a few workgroups per long recording when the batch is small */
+        const int64_t gy = std::min<int64_t>((((maxnd + 63) >> 6) + 3) / 4, std::max<int64_t>(1, 2048 / F));
+        LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F, (unsigned)gy), dim3(256), 0, s, bs);
+    }
     {
         QuantArgs a;
         a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
@@ -451,7 +455,9 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             LAUNCH(ctx, s, "k_rollq_fill", k_rollq_fill, dim3(4, (unsigned)F), dim3(256), 0, s, a);
             return BPMX_OK;
         };
-        const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, 8), F);
+        /* k_interp / k_floor_final stride over a recording with gx workgroups:
+         * 8, or more when the batch has few recordings */
+        const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, std::max<int64_t>(8, 2048 / F)), F);
         if (O->n_raw_troughs)
             HIP_TRY(hipMemcpyAsync(O->n_raw_troughs, d_nraw, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
         {

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void k_block_stats(BlockStatArgs A) {
     double *bmx = A.bmax + A.boff[f], *bmn = A.bmin + A.boff[f];
     const int lane = lane_id();
     const double INF = __builtin_inf();
-    for (int64_t b = wave_id(); b < nb; b += 4) {
+    for (int64_t b = (int64_t)blockIdx.y * 4 + wave_id(); b < nb; b += 4 * (int64_t)gridDim.y) {
         int64_t i = (b << 6) + lane;
         double v = i < n ? x[i] : __builtin_nan("");
         double mx = wave_max(i < n ? v : -INF);
