@@ -360,7 +360,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         a.skip = nullptr;
         a.stats = 1;
         LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-        if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(256), 0, s, a);
+        if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(1024), 0, s, a);
     }
 
     /* ---- FLOOR ---- */
@@ -383,7 +383,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.n_levels = 1; a.q[0] = P->noise_floor_q; a.slot[0] = 1 << Q_NOISE;
             a.skip = d_run1; a.stats = 0;
             LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-            if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, 1), dim3(256), 0, s, a);
+            if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, 1), dim3(1024), 0, s, a);
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
         const int64_t W = P->noise_window;

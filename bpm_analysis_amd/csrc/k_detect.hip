@@ -29,7 +29,8 @@
 namespace bpmx {
 
 /* ------------------------------------------------------------------------ */
-__global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
+constexpr int KQ_T = 1024;   /* long recordings: one workgroup per (recording, level), 16 waves */
+__global__ __launch_bounds__(KQ_T) void k_quantile(QuantArgs A) {
     const int f = blockIdx.x, l = blockIdx.y;
     if (f >= A.n_files || l >= A.n_levels || !A.active[f] || (A.skip && A.skip[f])) return;
     const int64_t n = A.doff[f + 1] - A.doff[f];
@@ -39,8 +40,8 @@ __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
     __shared__ unsigned int hist[256];
     __shared__ long long s_r;
     __shared__ int s_digit;
-    __shared__ unsigned long long s_min[4];
-    __shared__ long long s_cnt[4];
+    __shared__ unsigned long long s_min[KQ_T / 64];
+    __shared__ long long s_cnt[KQ_T / 64];
 
     const double q = A.q[l];
     const double vi = (double)(n - 1) * q;
@@ -49,9 +50,9 @@ __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
     uint64_t prefix = 0, mask = 0;
     long long r = lo;
     for (int shift = 56; shift >= 0; shift -= 8) {
-        hist[tid] = 0;
+        if (tid < 256) hist[tid] = 0;
         __syncthreads();
-        for (int64_t i = tid; i < n; i += 256) {
+        for (int64_t i = tid; i < n; i += KQ_T) {
             uint64_t k = f64_key(x[i]);
             if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
         }
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
     if (!top) {
         unsigned long long mn = ~0ull;
         long long cnt = 0;
-        for (int64_t i = tid; i < n; i += 256) {
+        for (int64_t i = tid; i < n; i += KQ_T) {
             uint64_t k = f64_key(x[i]);
             if (k <= prefix) cnt++;
             else if (k < mn) mn = k;
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(256) void k_quantile(QuantArgs A) {
         __syncthreads();
         unsigned long long m = s_min[0];
         long long c = 0;
-        for (int w = 0; w < 4; ++w) { m = s_min[w] < m ? s_min[w] : m; c += s_cnt[w]; }
+        for (int w = 0; w < KQ_T / 64; ++w) { m = s_min[w] < m ? s_min[w] : m; c += s_cnt[w]; }
         const double vb = (c > lo + 1) ? va : key_f64(m);
         res = np_lerp(va, vb, vi - (double)lo);
     }
