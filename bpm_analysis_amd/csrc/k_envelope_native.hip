@@ -407,6 +407,36 @@ __global__ __launch_bounds__(64) void k_native_blocks_gen(NatBlockArgs A) {
     const int j = tl.j0 + lane;
     const bool valid = lane < A.bt && j < tl.nb;
     double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0, x0 = 0;
+    if constexpr (DT == BPMX_DT_I16 && MULTI) {
+        /* int16 stereo: lane = block strides ds frames through global memory
+         * (64 cache lines per load instruction), so the tile's frames are
+         * first staged in LDS with coalesced dword loads (one stereo frame
+         * each); same frames, same arithmetic as frame_value */
+        if (A.channels == 2 && ((uintptr_t)A.pcm & 3) == 0) {
+            __shared__ uint32_t s_fr[NB_RCH * 512 + 1];
+            const int nvalid = (int)min((int64_t)A.bt, (int64_t)tl.nb - tl.j0);
+            const int nfr = nvalid * ds + 1;                 /* frames [s0, s0 + nvalid ds] */
+            const uint32_t *src = (const uint32_t *)A.pcm + tl.s0;
+            for (int k = lane; k < nfr; k += 64) s_fr[k] = src[k];
+            __syncthreads();
+            if (valid) {
+                const double *__restrict__ coef = A.tab + TB_COEF;
+                const uint32_t *fr = s_fr + lane * ds;
+                for (int i = 0; i <= ds; ++i) {
+                    const uint32_t w = fr[i];
+                    const double xv = ((double)(int16_t)(w & 0xFFFFu) + (double)(int16_t)(w >> 16)) / 2.0;
+                    const double *c = coef + i * 8;
+                    u0 = __builtin_fma(c[0], xv, u0); u1 = __builtin_fma(c[1], xv, u1);
+                    u2 = __builtin_fma(c[2], xv, u2); u3 = __builtin_fma(c[3], xv, u3);
+                    v0 = __builtin_fma(c[4], xv, v0); v1 = __builtin_fma(c[5], xv, v1);
+                    v2 = __builtin_fma(c[6], xv, v2); v3 = __builtin_fma(c[7], xv, v3);
+                    if (i == 0) x0 = xv;
+                }
+            }
+            nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+            return;
+        }
+    }
     if (valid) {
         const double *__restrict__ coef = A.tab + TB_COEF;
         const int64_t fb = tl.s0 + (int64_t)lane * ds;
