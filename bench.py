@@ -45,6 +45,11 @@ def parse():
     ap.add_argument("--options", type=int, default=0, help="bpmx_option bits (diagnostics; 0 = defaults)")
     ap.add_argument("--contexts", type=int, default=4,
                     help="side measurement: the batch split over K contexts on K streams (0: skip)")
+    ap.add_argument("--exact-steps", type=int, default=5,
+                    help="side measurement: steps with the input-dependent exact shortcuts off "
+                         "(BPMX_OPT_DRAFT_FULL | BPMX_OPT_ROLLQ_NOPRUNE; 0: skip)")
+    ap.add_argument("--parity-files", type=int, default=16,
+                    help="N > 1: files per rank checked against the oracle (N = 1 checks every file)")
     return ap.parse_args()
 
 
@@ -105,40 +110,101 @@ def pmc_traffic(mode: str, kernel: str, workload: str, launches_per_step: float)
     return None
 
 
-def cpu_baseline(mode: str, fs: int, n_frames: int, n_files: int, params: dict) -> dict:
-    """The CPU oracle (C restatement of the reference path) on a bounded sample, all host cores."""
-    from concurrent.futures import ThreadPoolExecutor
+def cpu_threads():
+    """(threads used, CPUs in this process's affinity mask, os.cpu_count()).
 
-    from oracle import oracle as O
+    The CPU leg runs one thread per CPU of the affinity mask, capped by
+    OMP_NUM_THREADS when that is set: the GPU pool sets it to the host-CPU
+    share of one GPU (16), and os.cpu_count() there shows the whole machine."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    d = O.derive(fs, params)
-    with ThreadPoolExecutor(cores) as ex:
-        pcms = list(ex.map(lambda f: O.synth(10_000 + f, n_frames, fs, 1), range(n_files)))
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(omp) if omp.isdigit() and int(omp) > 0 else aff
+    return max(1, min(aff, share)), aff, os.cpu_count() or aff
 
-    def one(pcm):
-        env = O.preprocess_ref(pcm, d) if mode == "reference" else O.preprocess_native(pcm, d)
-        fl, tr, _ = O.noise_floor(env, d, params)
-        return len(O.raw_peaks(env, fl, d, params))
 
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(cores) as ex:
-        list(ex.map(one, pcms))
-    dt = time.perf_counter() - t0
+def _cpu_model() -> str:
     cpu = platform.processor() or platform.machine()
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": n_files * n_frames / dt, "unit": "audio-samples/s", "cores": cores, "kind": "port",
-            "sample": f"{n_files} x {n_frames / fs:.0f} s {fs} Hz mono int16 synthetic recordings, {mode} mode, "
-                      f"oracle/bpmx_oracle.c on {cores} threads of {cpu}; {dt:.2f} s wall"}
+    return cpu
+
+
+def oracle_outputs(mode: str, fs: int, n_frames: int, seeds, params: dict, threads: int):
+    """The oracle (C restatement of the reference path) on the recordings with
+    the given seeds: (per-file dicts, wall seconds of the detection itself).
+    Input synthesis is untimed; each worker drops its PCM after use."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    d = O.derive(fs, params)
+    with ThreadPoolExecutor(threads) as ex:
+        pcms = list(ex.map(lambda s: O.synth(int(s), n_frames, fs, 1), seeds))
+
+    def one(k):
+        pcm = pcms[k]
+        env = O.preprocess_ref(pcm, d) if mode == "reference" else O.preprocess_native(pcm, d)
+        fl, tr, flags = O.noise_floor(env, d, params)
+        pk = O.raw_peaks(env, fl, d, params)
+        pcms[k] = None
+        return {"env": env, "floor": fl, "troughs": tr, "peaks": pk, "flags": flags}
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(one, range(len(pcms))))
+    return outs, time.perf_counter() - t0
+
+
+def compare_outputs(gpu: list, cpu: list, exact_env: bool) -> dict:
+    """Per-file parity of the GPU batch against the oracle: every trough and
+    peak index and the fallback flags bit-exact; env and floor bit-exact in
+    reference mode, within 1e-9 x max|env| in native mode (north_star asks for
+    1e-5 relative).  Returns counts over files and the worst relative errors."""
+    n = len(cpu)
+    pe = te = fe = 0
+    env_rel = floor_rel = 0.0
+    bad = []
+    for f, (g, o) in enumerate(zip(gpu, cpu)):
+        scale = float(np.max(np.abs(o["env"]))) or 1.0
+        de = float(np.max(np.abs(g["env"] - o["env"]))) / scale
+        df = np.abs(g["floor"] - o["floor"])
+        df = float(np.nanmax(df)) / scale if np.any(np.isfinite(df)) else 0.0
+        if not np.array_equal(np.isnan(g["floor"]), np.isnan(o["floor"])):
+            df = float("inf")
+        env_rel, floor_rel = max(env_rel, de), max(floor_rel, df)
+        p_ok = np.array_equal(g["peaks"], o["peaks"])
+        t_ok = np.array_equal(g["troughs"], o["troughs"])
+        f_ok = (int(g["flags"]) & 7) == int(o["flags"])
+        pe += p_ok
+        te += t_ok
+        fe += f_ok
+        if not (p_ok and t_ok and f_ok) and len(bad) < 8:
+            bad.append(f)
+    tol = 0.0 if exact_env else 1e-9
+    return {"files": n, "peaks_equal": pe, "troughs_equal": te, "flags_equal": fe,
+            "env_max_rel": env_rel, "floor_max_rel": floor_rel, "env_tol": tol,
+            "ok": pe == n and te == n and fe == n and env_rel <= tol and floor_rel <= tol,
+            "mismatched_files": bad}
+
+
+def cpu_baseline(mode: str, fs: int, n_frames: int, seed0: int, n_files: int, params: dict, gpu_host: list):
+    """The CPU oracle on exactly the GPU batch's recordings (seeds seed0 + f),
+    timed, and the GPU outputs compared against it file by file."""
+    threads, aff, ncpu = cpu_threads()
+    outs, dt = oracle_outputs(mode, fs, n_frames, [seed0 + f for f in range(n_files)], params, threads)
+    parity = compare_outputs(gpu_host[:n_files], outs, exact_env=(mode == "reference"))
+    base = {"value": n_files * n_frames / dt, "unit": "audio-samples/s", "cores": threads, "kind": "port",
+            "affinity_cpus": aff, "os_cpu_count": ncpu,
+            "sample": f"the GPU batch's own {n_files} recordings (seeds {seed0}..{seed0 + n_files - 1}, "
+                      f"{n_frames / fs:.0f} s {fs} Hz mono int16), {mode} mode, oracle/bpmx_oracle.c + numpy FFT "
+                      f"on {threads} threads of {_cpu_model()}; {dt:.2f} s wall"}
+    return base, parity
 
 
 def shard_seed0(rank: int, files_per_gpu: int) -> int:
@@ -251,6 +317,7 @@ def main():
     t1 = time.perf_counter()
     det.profile(False)
     prof = det.profile_read()
+    gpu_host = out.to_host()           # the timed steps' outputs (checked against the oracle below)
     elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
     slabs = gather_peak_slabs(peak_slab(out.peaks, torch.from_numpy(out.doff), out.n_peaks), world, rank)
     gathered = None
@@ -319,6 +386,48 @@ def main():
             x.close()
         del outs, views, streams
 
+    # Side measurement (never `value`): the same step with the two exact but
+    # input-dependent shortcuts off (draft-floor bracket, final-floor pruning),
+    # i.e. the step a recording that defeats them costs.  Outputs must not change.
+    exact = None
+    if args.exact_steps > 0:
+        import torch as _t
+        ref = [x.clone() for x in (out.floor, out.troughs, out.peaks, out.n_troughs, out.n_peaks, out.flags)]
+        opt = args.options | 8 | 16       # BPMX_OPT_DRAFT_FULL | BPMX_OPT_ROLLQ_NOPRUNE
+        det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=opt)
+        torch.cuda.synchronize()
+        te0 = time.perf_counter()
+        for _ in range(args.exact_steps):
+            det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=opt)
+        torch.cuda.synchronize()
+        edt = (time.perf_counter() - te0) / args.exact_steps
+        same = all(_t.equal(a, b) if a.dtype != _t.float64 else _t.equal(a.nan_to_num(-1.0), b.nan_to_num(-1.0))
+                   for a, b in zip(ref, (out.floor, out.troughs, out.peaks, out.n_troughs, out.n_peaks, out.flags)))
+        exact = {"options": opt, "value": F * n / edt, "unit": "audio-samples/s", "ms_per_step": edt * 1e3,
+                 "steps": args.exact_steps, "per_gpu": True, "outputs_identical": bool(same)}
+        del ref
+
+    # Parity of the timed batch against the oracle on the same recordings.  N = 1:
+    # every file, in the cpu_baseline leg below.  N > 1: a bounded sample of
+    # every rank's shard, counts summed over ranks.
+    parity = None
+    if world > 1 and args.parity_files > 0 and not args.no_cpu:
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        th = max(1, cpu_threads()[0] // max(1, lw))
+        pick = sorted(set(np.linspace(0, F - 1, min(F, args.parity_files)).astype(int).tolist()))
+        outs, _ = oracle_outputs(args.mode, fs, n, [shard_seed0(rank, F) + f for f in pick], params, th)
+        pr = compare_outputs([gpu_host[f] for f in pick], outs, exact_env=(args.mode == "reference"))
+        cnt = torch.tensor([pr["files"], pr["peaks_equal"], pr["troughs_equal"], pr["flags_equal"]],
+                           dtype=torch.float64, device=det.device)
+        worst = torch.tensor([pr["env_max_rel"], pr["floor_max_rel"]], dtype=torch.float64, device=det.device)
+        dist.all_reduce(cnt)
+        dist.all_reduce(worst, op=dist.ReduceOp.MAX)
+        c, w = cnt.tolist(), worst.tolist()
+        parity = {"files": int(c[0]), "ranks": world, "files_per_rank": len(pick), "peaks_equal": int(c[1]),
+                  "troughs_equal": int(c[2]), "flags_equal": int(c[3]), "env_max_rel": w[0], "floor_max_rel": w[1],
+                  "env_tol": pr["env_tol"],
+                  "ok": c[1] == c[0] and c[2] == c[0] and c[3] == c[0] and max(w) <= pr["env_tol"]}
+
     # Side measurement (never `value`): the host beat stages (beats.py: classifier,
     # refinement, BPM curve, metrics — SURVEY 8(f) rows 1 and 3) on the first
     # files of this batch's GPU outputs, one core.  Outside the north-star metric.
@@ -367,9 +476,9 @@ def main():
         pipeline = {"hbm_bytes_per_step": step_bytes, "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
                     "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
         cpu = None
-        if not args.no_cpu and args.cpu_files != 0:
-            nfc = args.cpu_files if args.cpu_files > 0 else min(F, 1024)
-            cpu = cpu_baseline(args.mode, fs, n, nfc, params)
+        if world == 1 and not args.no_cpu and args.cpu_files != 0:
+            nfc = args.cpu_files if args.cpu_files > 0 else F
+            cpu, parity = cpu_baseline(args.mode, fs, n, shard_seed0(rank, F), nfc, params, gpu_host)
         line = {
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -377,10 +486,11 @@ def main():
             "config": {"workload": workload,
                        "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
                        "parallelism": f"file-sharded x{world}"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
-            "result_gather": gathered, "multi_context": multi, "host_beat_stages": host_beats,
+            "result_gather": gathered, "multi_context": multi, "exact_no_shortcuts": exact,
+            "host_beat_stages": host_beats,
         }
         print(json.dumps(line))
     if world > 1:

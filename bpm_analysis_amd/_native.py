@@ -19,7 +19,7 @@ ABI_VERSION = 1
 DT_U8, DT_I16, DT_I32, DT_F32, DT_F64 = 0, 1, 2, 3, 4
 MODE_REFERENCE, MODE_NATIVE = 0, 1
 STAGE_ENVELOPE, STAGE_FLOOR, STAGE_PEAKS, STAGE_ALL = 1, 2, 4, 7
-F_STATIC_FLOOR, F_DRAFT_FLOOR, F_NAN_FLOOR, F_TOO_SHORT = 1, 2, 4, 8
+F_STATIC_FLOOR, F_DRAFT_FLOOR, F_NAN_FLOOR, F_TOO_SHORT, F_BAD_WINDOW = 1, 2, 4, 8, 16
 OPT_ROLLQ_MERGE = 1
 OPT_NATIVE_F64 = 2
 OPT_HILBERT_ROCFFT = 4
@@ -57,6 +57,12 @@ class Out(ctypes.Structure):
 
 class BpmxError(RuntimeError):
     pass
+
+
+class BpmxArgError(BpmxError, ValueError):
+    """BPMX_E_ARG: an argument the reference's own calls reject with ValueError
+    (scipy find_peaks' distance check, pandas' rolling-window checks); the
+    message is the library's, which repeats the reference-side wording."""
 
 
 _lib = None
@@ -101,4 +107,6 @@ def load() -> ctypes.CDLL:
 def check(rc: int, what: str) -> None:
     if rc != OK:
         msg = load().bpmx_last_error().decode(errors="replace")
+        if rc == E_ARG:
+            raise BpmxArgError(msg)
         raise BpmxError(f"{what} failed ({rc}): {msg}")

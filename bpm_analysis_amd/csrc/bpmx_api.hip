@@ -52,6 +52,13 @@ __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *ac
     for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
 }
 
+/* recordings with >= 5 raw troughs reach the rolling quantile: with a noise
+ * window below min_periods pandas raises there (bpm_analysis.py:1085) */
+__global__ __launch_bounds__(256) void k_flag_window(int n_files, const int32_t *run, int32_t *flags) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f < n_files && run[f]) flags[f] |= BPMX_F_BAD_WINDOW;
+}
+
 __global__ __launch_bounds__(64) void k_synth_beats(uint64_t seed0, int n_files, const int64_t *foff,
                                                     const int64_t *boff, int32_t fs, int64_t *s1, int64_t *s2,
                                                     int32_t *nb) {
@@ -235,8 +242,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     if (do_floor && !O->troughs) return fail(BPMX_E_ARG, "troughs array required");
     if (do_peaks && !O->peaks) return fail(BPMX_E_ARG, "peaks array required");
     if ((do_floor || do_peaks) && P->distance < 1) return fail(BPMX_E_ARG, "`distance` must be greater or equal to 1");
-    if (do_floor && (P->noise_window < P->min_periods || P->min_periods < 1))
-        return fail(BPMX_E_ARG, "min_periods must be <= noise window");
+    if (do_floor && P->min_periods < 1) return fail(BPMX_E_ARG, "min_periods must be >= 1");
+    /* noise window < min_periods: pandas' rolling() raises ValueError, but only
+     * for recordings that reach it (>= 5 troughs, :1073-1085); those get
+     * BPMX_F_BAD_WINDOW and the rest of the batch runs normally */
+    const bool bad_window = do_floor && P->noise_window < P->min_periods;
     if (do_env && P->env_window < 1) return fail(BPMX_E_ARG, "envelope window must be >= 1");
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
@@ -377,6 +387,9 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.run_out = d_run1; a.run_min = 5;
             LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
         }
+        if (bad_window)
+            LAUNCH(ctx, s, "k_flag_window", k_flag_window, dim3((F + 255) / 256), dim3(256), 0, s, F, d_run1,
+                   (int32_t *)O->flags);
         if (noise_lazy) {                 /* the static-floor quantile, for recordings with < 5 troughs */
             QuantArgs a;
             a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
@@ -386,7 +399,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, 1), dim3(1024), 0, s, a);
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
-        const int64_t W = P->noise_window;
+        const int64_t W = bad_window ? P->min_periods : P->noise_window;
         const int cap = (int)((W + RQ_T - 1 + 63) / 64 * 64);
         const size_t lds = rollq_lds_bytes(RQ_T, cap);
         /* wavelet-matrix kernel for recordings that fit its LDS budget; the

@@ -31,6 +31,21 @@ from .design import design
 from .engine import default_detector
 
 PADLEN_MSG = "The length of the input vector x must be greater than padlen, which is 15."
+DISTANCE_MSG = "`distance` must be greater or equal to 1"          # scipy find_peaks (:1070, :227)
+
+
+def _window_error(params: Dict, sample_rate: int) -> ValueError:
+    """pandas' rolling() check of the noise window (bpm_analysis.py:1084-1085)."""
+    return ValueError(f"min_periods 3 must be <= window {int(params['noise_window_sec'] * sample_rate)}")
+
+
+def _file_error(flags: int, params: Dict, sr: int):
+    """The exception the reference raises for a recording flagged by the library, or None."""
+    if flags & N.F_TOO_SHORT:
+        return ValueError(PADLEN_MSG)
+    if flags & N.F_BAD_WINDOW:
+        return _window_error(params, sr)
+    return None
 
 
 def _read_wav(file_path: str):
@@ -79,8 +94,12 @@ def _series(values: np.ndarray):
 def _calculate_dynamic_noise_floor(audio_envelope: np.ndarray, sample_rate: int, params: Dict, device: int = 0):
     """Calculates a dynamic noise floor based on a sanitized set of audio troughs (on the GPU)."""
     env = np.ascontiguousarray(audio_envelope, dtype=np.float64)
+    if int(params["min_peak_distance_sec"] * sample_rate) < 1:
+        raise ValueError(DISTANCE_MSG)
     r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_FLOOR)[0]
     fl = r["flags"]
+    if fl & N.F_BAD_WINDOW:
+        raise _window_error(params, sample_rate)
     if fl & N.F_STATIC_FLOOR:
         logging.warning("Not enough troughs found for sanitization. Using a static noise floor.")
         return _series(np.array(r["floor"])), np.array(r["troughs"], dtype=np.int64)
@@ -96,7 +115,7 @@ def find_raw_peaks(audio_envelope: np.ndarray, sample_rate: int, params: Dict, h
     """Finds all potential peaks above the given height threshold (on the GPU)."""
     env = np.ascontiguousarray(audio_envelope, dtype=np.float64)
     if int(params["min_peak_distance_sec"] * sample_rate) < 1:
-        raise ValueError("`distance` must be greater or equal to 1")
+        raise ValueError(DISTANCE_MSG)
     floor = np.ascontiguousarray(np.broadcast_to(np.asarray(height_threshold, dtype=np.float64), env.shape))
     r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor])[0]
     peaks = np.array(r["peaks"], dtype=np.int64)
@@ -159,10 +178,19 @@ def analyze_wav_files(file_paths: Sequence[str], params: Dict, output_directory:
             for k in idx:
                 out[k] = {"error": exc}
             continue
-        res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save)
+        try:
+            if d.distance < 1:
+                raise ValueError(DISTANCE_MSG)
+            res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save)
+        except (ValueError, N.BpmxError) as exc:      # reported per file, as the GUI loop does (gui.py:247-251)
+            for k in idx:                             # (a too-short file fails first, in filtfilt)
+                short = -(-audio[k][1].shape[0] // d.ds) <= 15
+                out[k] = {"error": ValueError(PADLEN_MSG) if short else exc}
+            continue
         for k, r in zip(idx, res):
-            if r["flags"] & N.F_TOO_SHORT:
-                out[k] = {"error": ValueError(PADLEN_MSG)}
+            err = _file_error(r["flags"], params, d.sr)
+            if err is not None:
+                out[k] = {"error": err}
                 continue
             if save:
                 path = file_paths[k]

@@ -66,7 +66,9 @@ enum bpmx_file_flag {
     BPMX_F_STATIC_FLOOR = 1, /* < 5 troughs: constant quantile floor, troughs unsanitised (:1073-1077) */
     BPMX_F_DRAFT_FLOOR = 2,  /* <= 2 sanitised troughs: draft floor kept (:1107-1110) */
     BPMX_F_NAN_FLOOR = 4,    /* all-NaN floor replaced by quantile(env, 0.1) (:1113-1115) */
-    BPMX_F_TOO_SHORT = 8     /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
+    BPMX_F_TOO_SHORT = 8,    /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
+    BPMX_F_BAD_WINDOW = 16   /* noise_window < min_periods and >= 5 troughs: pandas rolling() raises
+                                ValueError (:1085); floor/peaks of this recording are not meaningful */
 };
 
 enum bpmx_option {

@@ -82,3 +82,40 @@ def test_reference_side_stub_matches_package():
         p1 = stub.make_params(fs, DEFAULT_PARAMS)
         p2 = make_params(design(fs, DEFAULT_PARAMS, log=False), DEFAULT_PARAMS, 0, 7, 1, 1)
         assert bytes(p1) == bytes(p2)
+
+
+def test_patch_reference_rebinds_the_hot_path_names():
+    """patch_reference points a reference module's three hot-path names at the
+    drop-ins (what runs behind them is the GPU test's business)."""
+    import types
+
+    from bpm_analysis_amd import dropin
+
+    class PeakClassifier:
+        def _find_raw_peaks(self, height_threshold):
+            raise AssertionError("unpatched")
+
+    mod = types.ModuleType("stand_in")
+    mod.preprocess_audio = mod._calculate_dynamic_noise_floor = None
+    mod.PeakClassifier = PeakClassifier
+    dropin.patch_reference(mod)
+    assert mod.preprocess_audio is dropin.preprocess_audio
+    assert mod._calculate_dynamic_noise_floor is dropin._calculate_dynamic_noise_floor
+    assert PeakClassifier._find_raw_peaks.__name__ == "_find_raw_peaks"
+    assert PeakClassifier._find_raw_peaks is not None and "unpatched" not in str(PeakClassifier._find_raw_peaks)
+
+
+def test_arg_errors_are_value_errors():
+    """BPMX_E_ARG surfaces as ValueError (the reference's exception type)."""
+    assert issubclass(N.BpmxArgError, ValueError) and issubclass(N.BpmxArgError, N.BpmxError)
+    from bpm_analysis_amd import dropin
+    e = dropin._window_error({"noise_window_sec": 0.005}, 302)
+    assert isinstance(e, ValueError) and str(e) == "min_periods 3 must be <= window 1"
+    import pandas as pd
+    with pytest.raises(ValueError, match=str(e)):
+        pd.Series(np.arange(10.0)).rolling(window=1, min_periods=3, center=True)
+    with pytest.raises(ValueError, match=str(dropin._window_error({"noise_window_sec": -1.0}, 302))):
+        pd.Series(np.arange(10.0)).rolling(window=-302, min_periods=3, center=True)
+    from scipy.signal import find_peaks
+    with pytest.raises(ValueError, match=dropin.DISTANCE_MSG):
+        find_peaks(np.arange(10.0), distance=0)

@@ -157,19 +157,21 @@ def test_native_ragged_batch(det):
         _check_file(r, g, exact_env=False)
 
 
-@pytest.mark.parametrize("fs,lens,shift", [
-    (44100, [44100 * 7 + 3, 44100 * 5 + 1, 146 * 16 + 7, 44100 * 3], 0),   # odd file offsets, tiny file
-    (96000, [96000 * 6 + 5, 96000 * 4], 0),                               # ds = 300: 34-block tiles
-    (44100, [44100 * 6 + 1, 44100 * 4 + 2], 1),                           # pcm not 16-B aligned: generic path
+@pytest.mark.parametrize("fs,lens,shift,ch", [
+    (44100, [44100 * 7 + 3, 44100 * 5 + 1, 146 * 16 + 7, 44100 * 3], 0, 1),   # odd file offsets, tiny file
+    (96000, [96000 * 6 + 5, 96000 * 4], 0, 1),                               # ds = 300: 34-block tiles
+    (44100, [44100 * 6 + 1, 44100 * 4 + 2], 1, 1),                           # pcm not 16-B aligned: generic path
+    (48000, [48000 * 5 + 3, 48000 * 3 + 1], 1, 2),                           # stereo, not 4-B aligned: generic path
+    (44100, [44100 * 4 + 2, 44100 * 3 + 5], 0, 3),                           # three channels: generic path
 ])
-def test_native_tile_geometries(det, fs, lens, shift):
+def test_native_tile_geometries(det, fs, lens, shift, ch):
     import torch
-    recs = [O.synth(500 + i, n, fs, 1) for i, n in enumerate(lens)]
-    flat = np.concatenate([np.zeros(shift, np.int16)] + recs)
+    recs = [O.synth(500 + i, n, fs, ch) for i, n in enumerate(lens)]
+    flat = np.concatenate([np.zeros(shift, np.int16)] + [r.reshape(-1) for r in recs])
     dev = torch.from_numpy(flat).to(det.device)[shift:]
     fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     params = dict(G.BASE_PARAMS)
-    res = det.run(dev, fo, fs, params, mode="native", want_y=True)
+    res = det.run(dev, fo, fs, params, mode="native", want_y=True, channels=ch)
     torch.cuda.synchronize()
     for h, pcm in zip(res.to_host(), recs):
         o = O.detect(pcm, fs, params, mode="native")
@@ -482,3 +484,115 @@ def test_draft_bounds_window_ranking(det, secs):
         assert _same(r["floor"], want["floor"])
         assert _same(r["troughs"], want["troughs"])
         assert _same(r["peaks"], want["peaks"])
+
+
+def _stand_in_reference():
+    """A minimal stand-in for the reference module: the three hot-path names
+    (unpatched they raise) and a PeakClassifier whose constructor runs
+    _initialize_state the way bpm_analysis.py:80-91 does, plus the first stages
+    of analyze_wav_file (:1731-1740)."""
+    import types
+    mod = types.ModuleType("bpm_analysis_stand_in")
+
+    def unpatched(*a, **k):
+        raise AssertionError("reference hot path called: patch_reference did not rebind it")
+
+    class PeakClassifier:
+        def __init__(self, audio_envelope, sample_rate, params, start_bpm_hint, precomputed_noise_floor,
+                     precomputed_troughs, peak_bpm_time_sec, recovery_end_time_sec):
+            self.audio_envelope = audio_envelope
+            self.sample_rate = sample_rate
+            self.params = params
+            self.state = self._initialize_state(start_bpm_hint, precomputed_noise_floor, precomputed_troughs)
+
+        def _initialize_state(self, start_bpm_hint, precomputed_noise_floor, precomputed_troughs):
+            state = {"analysis_data": {}}
+            state["dynamic_noise_floor"], state["trough_indices"] = precomputed_noise_floor, precomputed_troughs
+            state["all_peaks"] = self._find_raw_peaks(state["dynamic_noise_floor"].values)
+            return state
+
+        _find_raw_peaks = unpatched
+
+    def analyze_wav_file(wav_file_path, params, start_bpm_hint, original_file_path, output_directory):
+        env, sr = mod.preprocess_audio(wav_file_path, params, output_directory)
+        floor, troughs = mod._calculate_dynamic_noise_floor(env, sr, params)
+        pc = mod.PeakClassifier(env, sr, params, start_bpm_hint, floor, troughs, None, None)
+        return env, floor, troughs, pc.state["all_peaks"]
+
+    mod.preprocess_audio = unpatched
+    mod._calculate_dynamic_noise_floor = unpatched
+    mod.PeakClassifier = PeakClassifier
+    mod.analyze_wav_file = analyze_wav_file
+    return mod
+
+
+def test_patch_reference_runs_the_reference_entry_on_the_gpu(det, tmp_path):
+    """dropin.patch_reference rebinds a reference module's hot path; the
+    module's own entry point then runs it through libbpmx.so (bit-exact)."""
+    from scipy.io import wavfile
+    from bpm_analysis_amd import dropin
+    mod = _stand_in_reference()
+    dropin.patch_reference(mod)
+    g = G.load("ref_44k_60s_mono")
+    wav = tmp_path / "rec.wav"
+    wavfile.write(str(wav), int(g["fs"]), g["pcm"])
+    params = dict(g["params"], save_filtered_wav=False)
+    env, floor, troughs, peaks = mod.analyze_wav_file(str(wav), params, None, str(wav), str(tmp_path))
+    assert _same(env, g["env"]) and _same(floor.values, g["floor"])
+    assert _same(troughs, g["troughs"]) and _same(peaks, g["peaks"])
+
+
+def test_reference_value_errors(det, tmp_path):
+    """The reference's ValueErrors at the boundary: scipy's distance check, and
+    pandas' rolling-window check, which fires only for recordings that reach
+    the rolling quantile (>= 5 troughs); per file in the batched entry."""
+    from scipy.io import wavfile
+    import bpm_analysis_amd as B
+    from bpm_analysis_amd import dropin
+    g = G.load("ref_44k_60s_mono")
+    env, sr = g["env"], int(g["sr"])
+    with pytest.raises(ValueError, match="min_periods 3 must be <= window 1"):
+        B._calculate_dynamic_noise_floor(env, sr, dict(g["params"], noise_window_sec=0.005))
+    with pytest.raises(ValueError, match="min_periods 3 must be <= window -302"):
+        B._calculate_dynamic_noise_floor(env, sr, dict(g["params"], noise_window_sec=-1.0))
+    with pytest.raises(ValueError, match="`distance` must be greater or equal to 1"):
+        B._calculate_dynamic_noise_floor(env, sr, dict(g["params"], min_peak_distance_sec=0.001))
+    # < 5 troughs: the static floor is returned before the window is used
+    s = G.load("env_static_fallback")
+    fl, tr = B._calculate_dynamic_noise_floor(s["env"], int(s["sr"]), dict(s["params"], noise_window_sec=0.005))
+    assert _same(fl.values, s["floor"]) and _same(tr, s["troughs"])
+    # a library E_ARG is a ValueError too
+    from bpm_analysis_amd import _native as N
+    with pytest.raises(ValueError):
+        det.run_env_host([env], sr, dict(g["params"], min_peak_distance_sec=0.001), N.STAGE_PEAKS, floors=[env])
+    paths = []
+    for name, pcm in [("a.wav", g["pcm"]), ("b.wav", O.synth(3, 146 * 15, 44100, 1))]:
+        paths.append(str(tmp_path / name))
+        wavfile.write(paths[-1], 44100, pcm)
+    res = dropin.analyze_wav_files(paths, dict(g["params"], noise_window_sec=0.005), str(tmp_path))
+    assert "min_periods 3" in str(res[0]["error"]) and "padlen" in str(res[1]["error"])
+    res = dropin.analyze_wav_files(paths, dict(g["params"], min_peak_distance_sec=0.001), str(tmp_path))
+    assert "distance" in str(res[0]["error"]) and "padlen" in str(res[1]["error"])
+
+
+def test_native_batch_at_c3_scale(det):
+    """BASELINE config C3: 256 x 60 s 44.1 kHz mono recordings in one native-mode
+    batch generated in HBM; 16 of them re-derived by the oracle (indices exact,
+    envelope/floor within 1e-9 of max|env|), all of them checked for the
+    find_peaks invariants."""
+    import torch
+    fs, F, n = 44100, 256, 44100 * 60
+    fo = np.arange(F + 1, dtype=np.int64) * n
+    pcm = det.synth(fo, fs, 1, seed0=5000)
+    params = dict(G.BASE_PARAMS)
+    res = det.run(pcm, fo, fs, params, mode="native")
+    torch.cuda.synchronize()
+    host = res.to_host()
+    del pcm
+    for f in np.linspace(0, F - 1, 16).astype(int):
+        o = O.detect(O.synth(5000 + int(f), n, fs, 1), fs, params, mode="native")
+        _check_file(host[f], o, exact_env=False)
+    for h in host:
+        pk, env, fl, tr = h["peaks"], h["env"], h["floor"], h["troughs"]
+        assert len(pk) > 100 and np.all(np.diff(pk) >= 15) and np.all(np.diff(tr) >= 15)
+        assert np.all(env[pk] >= fl[pk]) and h["flags"] == 0
