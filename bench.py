@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--exact-steps", type=int, default=5,
                     help="side measurement: steps with the input-dependent exact shortcuts off "
                          "(BPMX_OPT_DRAFT_FULL | BPMX_OPT_ROLLQ_NOPRUNE; 0: skip)")
+    ap.add_argument("--workload", default="metric", choices=["metric", "c5"],
+                    help="metric: BASELINE's headline (1024 x 60 s 44.1 kHz mono per GPU); c5: BASELINE config C5, "
+                         "64 x U[10, 30] min 96 kHz stereo per GPU (512 over 8 GPUs), ragged, LPT over ranks")
     ap.add_argument("--parity-files", type=int, default=16,
                     help="N > 1: files per rank checked against the oracle (N = 1 checks every file)")
     return ap.parse_args()
@@ -56,33 +59,38 @@ def parse():
 def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, channels: int = 1) -> dict:
     """Algorithmic HBM bytes PER STEP of each kernel label (summed over its
     launches in one step): the bytes the algorithm must
-    move, not what the implementation happens to move."""
-    F = n_files
-    nb = nd - 1
+    move, not what the implementation happens to move.  Uniform lengths."""
+    return algorithmic_bytes_total(mode, n_files, n_files * n_frames, n_files * nd, channels)
+
+
+def algorithmic_bytes_total(mode: str, F: int, frames: int, nd: int, channels: int = 1) -> dict:
+    """The same for a ragged batch: F recordings, `frames` frames and `nd`
+    decimated samples in total."""
+    nb = nd - F
     common = {
-        "k_quantile": F * nd * 8,                          # env read once
-        "k_quantile_reg": F * nd * 8,
-        "k_block_stats": F * nd * 8,
-        "k_find_peaks[troughs]": F * nd * 8,
-        "k_find_peaks[peaks]": F * nd * 16,                # env + floor
-        "k_draft_bounds": F * 240 * 16,                    # ~240 raw troughs x (position, value) + decisions
+        "k_quantile": nd * 8,                          # env read once
+        "k_quantile_reg": nd * 8,
+        "k_block_stats": nd * 8,
+        "k_find_peaks[troughs]": nd * 8,
+        "k_find_peaks[peaks]": nd * 16,                # env + floor
+        "k_draft_bounds": nd // 76 * 16,               # ~1 raw trough per 76 samples x (position, value)
         # final floor: dense (interpolated in-kernel from the troughs) in, floor out; the
         # draft pass runs only for recordings with an undecided trough (none on this workload)
-        "k_rollq_wm": F * nd * 8,
-        "k_rollq_wm[full]": 0,                              # unpruned variant: recordings the pruned one flags (none here)
+        "k_rollq_wm": nd * 8,
+        "k_rollq_wm[full]": 0,                          # unpruned variant: recordings the pruned one flags (none here)
         "k_init_out": 0,
-        "k_rolling_quantile": F * nd * 16,
+        "k_rolling_quantile": nd * 16,
         "k_floor_final": 0, "k_sanitize": 0, "k_interp": 0,
     }
     if mode == "native":
         return dict(common, **{
-            "k_native_blocks": F * n_frames * channels * 2,      # every PCM sample read once (SURVEY 8(d))
-            "k_native_carry": F * (nb // 64 * 128 + 64 * 16 * 8),  # tile carries in/out, partial tile
-            "k_native_yd": F * nb * (8 + 8),                          # gamma in, yd out
-            "k_hilbert_env": F * nd * (8 + 8),                        # yd in, env out (transform in LDS)
+            "k_native_blocks": frames * channels * 2,                 # every PCM sample read once (SURVEY 8(d))
+            "k_native_carry": nb // 64 * 128 + F * 64 * 16 * 8,       # tile carries in/out, partial tile
+            "k_native_yd": nb * (8 + 8),                              # gamma in, yd out
+            "k_hilbert_env": nd * (8 + 8),                            # yd in, env out (transform in LDS)
         })
     # reference: the picked samples, y kept in scratch (written fwd, rewritten bwd, read twice), env written once
-    return dict(common, **{"k_envelope_ref": F * (nd * channels * 2 + (nd + 30) * 8 * 4 + nd * 8)})
+    return dict(common, **{"k_envelope_ref": nd * channels * 2 + (nd + 30 * F) * 8 * 4 + nd * 8})
 
 
 # launch labels -> kernel names in the rocprofv3 PMC summary
@@ -229,37 +237,116 @@ def reduce_results(elapsed: float, n_peaks, world: int, rank: int):
     return float(tt.item()), total
 
 
-def peak_slab(peaks, doff, counts):
-    """Per-file raw-peak indices as a padded [files, cap] int32 slab (-1 pads):
-    the fixed-size record each shard hands to the final result gather."""
-    import torch
-    cap = int(counts.max().item()) if counts.numel() else 0
-    cap = max(cap, 1)
-    ar = torch.arange(cap, device=peaks.device, dtype=torch.int64)
-    start = doff[:-1].to(peaks.device).unsqueeze(1)
-    idx = (start + ar.unsqueeze(0)).clamp(max=peaks.numel() - 1)
-    slab = peaks[idx].to(torch.int32)
-    return torch.where(ar.unsqueeze(0) < counts.to(peaks.device).long().unsqueeze(1), slab,
-                       torch.full_like(slab, -1))
+def c5_lengths(n_files: int, fs: int = 96000, seed: int = 2025):
+    """BASELINE config C5: recordings of U[10, 30] minutes (whole seconds), seeded."""
+    rng = np.random.default_rng(seed)
+    return (rng.integers(600, 1801, size=n_files) * fs).astype(np.int64)
 
 
-def gather_peak_slabs(slab, world: int, rank: int):
-    """The final result gather: every shard's padded peak slab to
-    rank 0 over RCCL (gloo in the CPU tests); slabs are padded to the widest
-    shard first.  Returns the list of slabs on rank 0, None elsewhere."""
+def run_c5(args):
+    """Side workload (never the driver's headline): BASELINE config C5, 64
+    ragged 10-30 min 96 kHz stereo recordings per GPU (512 on 8 GPUs),
+    native mode.  Recordings are placed over ranks by shard.lpt_partition of
+    the frame counts (every rank derives the same placement), each rank
+    synthesises its own in HBM (seed = global recording index) and runs them
+    longest first in one ragged batch.  Prints one JSON line."""
     import torch
     import torch.distributed as dist
-    if world <= 1:
-        return [slab]
-    w = torch.tensor([slab.shape[1]], dtype=torch.int64, device=slab.device)
-    dist.all_reduce(w, op=dist.ReduceOp.MAX)
-    cap = int(w.item())
-    if slab.shape[1] < cap:
-        pad = torch.full((slab.shape[0], cap - slab.shape[1]), -1, dtype=slab.dtype, device=slab.device)
-        slab = torch.cat([slab, pad], dim=1)
-    out = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
-    dist.gather(slab.contiguous(), out, dst=0)
-    return out
+
+    from bpm_analysis_amd import DEFAULT_PARAMS
+    from bpm_analysis_amd.design import design
+    from bpm_analysis_amd.engine import Detector
+    from bpm_analysis_amd.shard import FileResult, gather_file_results, lpt_partition
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    det = Detector(local)
+    params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
+    fs, ch, per = 96000, 2, 64
+    lengths = c5_lengths(per * world, fs)
+    mine = lpt_partition(lengths, world)[rank]
+    fo = np.concatenate([[0], np.cumsum(lengths[mine])]).astype(np.int64)
+    d = design(fs, params, log=False)
+    pcm = det.synth(fo, fs, ch, seeds=[100_000 + i for i in mine])
+    out = det.alloc(fo, d.ds, d.sr)
+    frames = int(fo[-1])
+    nd_tot = int(out.doff[-1])
+
+    def step():
+        det.run(pcm, fo, fs, params, mode="native", channels=ch, out=out, d=d, options=args.options)
+
+    abytes = algorithmic_bytes_total("native", len(mine), frames, nd_tot, ch)
+    det.profile(True)
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    det.profile(False)
+    kprof = det.profile_read()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    host = out.to_host()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=det.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # parity: this rank's two shortest recordings against the oracle (bounded CPU time)
+    parity = None
+    if not args.no_cpu:
+        from oracle import oracle as O
+        pick = sorted(range(len(mine)), key=lambda k: lengths[mine[k]])[:2]
+        outs = []
+        for k in pick:
+            o = O.detect(O.synth(100_000 + mine[k], int(lengths[mine[k]]), fs, ch), fs, params, mode="native")
+            outs.append({kk: o[kk] for kk in ("env", "floor", "troughs", "peaks", "flags")})
+        parity = compare_outputs([host[k] for k in pick], outs, exact_env=False)
+        parity["files_checked"] = [int(mine[k]) for k in pick]
+    rows = [FileResult(int(i), raw_peaks=host[k]["peaks"], flags=host[k]["flags"]) for k, i in enumerate(mine)]
+    allres = gather_file_results(rows, len(lengths), device=det.device if world > 1 else None)
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        total = int(lengths.sum()) * ch
+        kernels = {k: {"launches": c, "avg_ms": round(t / c, 4), "share": round(t / max(1, args.warmup) / ms, 4)}
+                   for k, (c, t) in sorted(kprof.items())}
+        roof = None
+        if "k_native_blocks" in kprof:
+            c, t = kprof["k_native_blocks"]
+            kms = t / max(1, args.warmup)
+            ach = abytes["k_native_blocks"] / (kms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_native_blocks",
+                    "kernel_ms_per_step": round(kms, 4), "algorithmic_bytes_per_step": abytes["k_native_blocks"]}
+        step_bytes = frames * ch * 2
+        line = {"metric": "audio-samples/sec (filter+envelope+peaks), C5: 512 x 10-30 min 96 kHz stereo over 8 GPUs",
+                "value": total / (elapsed / args.steps), "unit": "audio-samples/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+                "config": {"workload": f"C5 shard: {per} x U[10,30] min 96000 Hz stereo int16 per GPU "
+                                       f"({per * world} recordings, LPT over {world} ranks), native mode",
+                           "recordings_rank0": len(mine), "frames_rank0": frames,
+                           "decimated_rank0": nd_tot, "parallelism": f"file-sharded x{world}"},
+                "roofline": roof,
+                "pipeline": {"hbm_bytes_per_step": step_bytes,
+                             "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
+                             "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
+                "parity": parity, "kernels": kernels,
+                "result_gather": {"files": sum(1 for r in allres if r is not None),
+                                  "peaks": int(sum(len(r["raw_peaks"]) for r in allres if r is not None))}}
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -319,12 +406,6 @@ def main():
     prof = det.profile_read()
     gpu_host = out.to_host()           # the timed steps' outputs (checked against the oracle below)
     elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
-    slabs = gather_peak_slabs(peak_slab(out.peaks, torch.from_numpy(out.doff), out.n_peaks), world, rank)
-    gathered = None
-    if rank == 0:
-        gathered = {"ranks": len(slabs), "files": int(sum(s.shape[0] for s in slabs)),
-                    "bytes": int(sum(s.numel() * 4 for s in slabs)),
-                    "peaks": int(sum(int((s >= 0).sum()) for s in slabs))}
     # per-kernel table from a separate, untimed pass with every launch bracketed
     det.profile_only("")
     det.profile(True)
@@ -431,16 +512,34 @@ def main():
     # Side measurement (never `value`): the host beat stages (beats.py: classifier,
     # refinement, BPM curve, metrics — SURVEY 8(f) rows 1 and 3) on the first
     # files of this batch's GPU outputs, one core.  Outside the north-star metric.
+    # Every rank's files then go to rank 0 in the final result gather (SURVEY
+    # 8(e)): raw peaks of every file, and final beats + the smoothed BPM curve of
+    # the files whose beat stages ran.
+    from bpm_analysis_amd.shard import FileResult, gather_file_results
+    rows = [FileResult(rank * F + f, raw_peaks=gpu_host[f]["peaks"], flags=gpu_host[f]["flags"]) for f in range(F)]
     host_beats = None
-    if rank == 0 and args.host_beat_files > 0:
+    if args.host_beat_files > 0:
         from bpm_analysis_amd import beats
-        res = out.to_host()[:args.host_beat_files]
+        res = gpu_host[:args.host_beat_files]
         th0 = time.perf_counter()
         done = beats.analyze_many(res, params)
         hdt = time.perf_counter() - th0
+        for f, a in enumerate(done):
+            if "error" not in a:
+                rows[f] = FileResult.from_analysis(rank * F + f, res[f]["peaks"], res[f]["flags"], a)
         host_beats = {"files": len(res), "cores": 1, "files_per_s": len(res) / hdt,
                       "audio_samples_per_s": len(res) * n / hdt, "ms_per_file": hdt / len(res) * 1e3,
                       "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))}
+    tg0 = time.perf_counter()
+    allres = gather_file_results(rows, world * F, device=det.device if world > 1 else None)
+    gathered = None
+    if rank == 0:
+        got = [r for r in allres if r is not None]
+        gathered = {"ranks": world, "files": len(got), "peaks": int(sum(len(r["raw_peaks"]) for r in got)),
+                    "bpm_curves": int(sum(1 for r in got if len(r["bpm"]))),
+                    "bpm_points": int(sum(len(r["bpm"]) for r in got)),
+                    "final_beats": int(sum(len(r["final_peaks"]) for r in got)),
+                    "ms": round((time.perf_counter() - tg0) * 1e3, 2)}
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -498,4 +597,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if parse().workload == "c5":
+        run_c5(parse())
+    else:
+        main()

@@ -171,15 +171,20 @@ class Detector:
                                     self.stream_handle()), "bpmx_run")
         return out
 
-    def synth(self, frame_offsets: Sequence[int], fs: int, channels: int = 1, seed0: int = 0):
-        """Synthetic int16 batch generated in HBM (bit-identical to bpmx_synth_host)."""
+    def synth(self, frame_offsets: Sequence[int], fs: int, channels: int = 1, seed0: int = 0,
+              seeds: Optional[Sequence[int]] = None):
+        """Synthetic int16 batch generated in HBM (bit-identical to bpmx_synth_host):
+        recording f gets seed ``seed0 + f``, or ``seeds[f]`` when given."""
         torch = _torch()
         fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
         pcm = torch.empty(int(fo[-1]) * channels, dtype=torch.int16, device=self.device)
+        runs = [(seed0, 0, len(fo) - 1)] if seeds is None else [(int(sd), f, f + 1) for f, sd in enumerate(seeds)]
         with self.lock:
-            N.check(self.L.bpmx_synth(self.ctx, seed0, len(fo) - 1, fo.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                      fs, channels, ctypes.c_void_p(pcm.data_ptr()), self.stream_handle()),
-                    "bpmx_synth")
+            for sd, a, b in runs:
+                sub = np.ascontiguousarray(fo[a:b + 1])
+                N.check(self.L.bpmx_synth(self.ctx, sd, b - a, sub.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                          fs, channels, ctypes.c_void_p(pcm.data_ptr()), self.stream_handle()),
+                        "bpmx_synth")
         return pcm
 
     def profile(self, on: bool):

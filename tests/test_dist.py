@@ -21,15 +21,14 @@ def _worker(rank, world, port, q):
     import bench
     counts = torch.arange(4, dtype=torch.int32) + 10 * rank      # per-file peak counts of this shard
     elapsed, total = bench.reduce_results(1.0 + rank, counts, world, rank)
-    # padded peak slabs: file f of rank r holds peaks 100*r + f*1000 + [0, counts[f])
-    doff = torch.tensor([0, 50, 100, 150, 200], dtype=torch.int64)
-    peaks = torch.full((200,), -7, dtype=torch.int64)
-    for f in range(4):
-        peaks[doff[f]:doff[f] + counts[f]] = 100 * rank + 1000 * f + torch.arange(int(counts[f]))
-    slabs = bench.gather_peak_slabs(bench.peak_slab(peaks, doff, counts), world, rank)
+    # result gather: file f of rank r holds peaks 100*r + f*1000 + [0, counts[f])
+    from bpm_analysis_amd.shard import FileResult, gather_file_results
+    rows = [FileResult(4 * rank + f, raw_peaks=100 * rank + 1000 * f + torch.arange(int(counts[f])).numpy())
+            for f in range(4)]
+    got = gather_file_results(rows, 4 * world)
     summary = None
     if rank == 0:
-        summary = [[row[row >= 0].tolist() for row in s] for s in slabs]
+        summary = [[got[4 * r + f]["raw_peaks"].tolist() for f in range(4)] for r in range(world)]
     q.put((rank, elapsed, total, bench.shard_seed0(rank, 4), summary))
     dist.destroy_process_group()
 
@@ -107,3 +106,76 @@ def test_two_rank_lpt_placement():
         assert list(n[part]) == sorted(n[part], reverse=True)
     assert list(longest_first([3, 5, 5, 1])) == [1, 2, 0, 3]     # stable among equal lengths
     assert lpt_partition([7, 7, 7, 7], 2) == [[0, 2], [1, 3]]
+
+
+class _OracleDetector:
+    """Test double for engine.Detector on CPU ranks: the oracle computes the hot
+    path so the gloo test exercises placement, the host beat stages and the
+    gather (the GPU detector is covered by the -m gpu tests)."""
+    device = torch.device("cpu")
+
+    def run_host(self, recs, fs, params, mode="native", stages=7):
+        from oracle import oracle as O
+        ds = O.derive(fs, params).ds
+        out = []
+        for r in recs:
+            if -(-len(r) // ds) <= 15:                  # the library's BPMX_F_TOO_SHORT, in both modes
+                out.append({"flags": 8})
+                continue
+            o = O.detect(r, fs, params, mode=mode)
+            out.append({k: o[k] for k in ("env", "floor", "troughs", "peaks", "sr", "flags")})
+        return out
+
+
+def _sharded_items():
+    from oracle import oracle as O
+    lens = [44100 * s for s in (25, 12, 31, 18, 9, 22)] + [146 * 15]          # ragged; the last is too short
+    return [O.synth(40 + i, n, 44100, 1) for i, n in enumerate(lens)]
+
+
+def _sharded_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bpm_analysis_amd import DEFAULT_PARAMS
+    from bpm_analysis_amd.shard import lpt_partition, run_sharded
+    items = _sharded_items()
+    params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
+    res = run_sharded(items, params, fs=44100, mode="native", detector=_OracleDetector())
+    q.put((rank, res, lpt_partition([len(x) for x in items], world)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_runner_gathers_peaks_and_bpm_curves():
+    """shard.run_sharded over 2 gloo ranks: LPT placement, per-rank detection
+    and host beat stages, and the rank-0 gather of raw peaks, final beats and
+    the smoothed BPM curve, equal to the single-process result file by file."""
+    import numpy as np
+    from bpm_analysis_amd import DEFAULT_PARAMS, beats
+    from oracle import oracle as O
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    outs = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, res, parts), (_, res1, _) = outs
+    assert res1 is None and len(res) == 7
+    params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
+    for i, pcm in enumerate(_sharded_items()):
+        r = res[i]
+        assert r["rank"] == (0 if i in parts[0] else 1)
+        if i == 6:
+            assert isinstance(r["error"], ValueError) and "padlen" in str(r["error"])
+            continue
+        o = O.detect(pcm, 44100, params, mode="native")
+        a = beats.analyze_recording(o["env"], o["sr"], o["floor"], o["troughs"], o["peaks"], params)
+        m = a["final_metrics"]
+        assert np.array_equal(r["raw_peaks"], o["peaks"])
+        assert np.array_equal(r["final_peaks"], a["final_peaks"])
+        assert np.array_equal(r["bpm_times"], np.asarray(m["bpm_times"]))
+        assert np.array_equal(r["bpm"], m["smoothed_bpm"].values)
+        assert r["flags"] == o["flags"] and len(r["bpm"]) > 5

@@ -18,6 +18,7 @@ for step in "$@"; do
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    c5) run bench_c5 600 python bench.py --workload c5 --steps 5 --warmup 2 ;;
     bench_ref) run bench_ref 600 python bench.py --steps 10 --warmup 2 --mode reference ;;
     rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 ;;
     rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --mode reference ;;
