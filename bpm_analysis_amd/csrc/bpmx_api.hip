@@ -404,11 +404,16 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         const size_t lds = rollq_lds_bytes(RQ_T, cap);
         /* wavelet-matrix kernel for recordings that fit its LDS budget; the
          * sorted-union kernel for longer ones (or when forced) */
-        const bool use_wm = !(P->options & BPMX_OPT_ROLLQ_MERGE);
+        const bool use_wm = !(P->options & (BPMX_OPT_ROLLQ_MERGE | BPMX_OPT_ROLLQ_GLOBAL));
         const bool need_merge = !use_wm || maxnd > WM_MMAX;
-        if (need_merge && (cap > 32 * RQ_T || W + RQ_T >= 65000))
-            return fail(BPMX_E_LIMIT, "noise window of " + std::to_string(W) +
-                                          " samples exceeds the rolling-quantile kernel (max 7800)");
+        /* windows beyond the LDS sorted-union kernel: the same algorithm with
+         * the union in global scratch (any window, any length) */
+        const bool merge_g = need_merge && (cap > 32 * RQ_T || W + RQ_T >= 65000 || (P->options & BPMX_OPT_ROLLQ_GLOBAL));
+        const int64_t gcap = (std::min<int64_t>(W + RQ_T, maxnd + 64) + 63) / 64 * 64;
+        const size_t lds_g = rollq_g_lds_bytes(RQ_T, gcap);
+        if (merge_g && lds_g > 160 * 1024)
+            return fail(BPMX_E_LIMIT, "noise window and recording both longer than " +
+                                          std::to_string((160 * 1024 - 16384) / 4 * 64) + " samples");
         uint16_t *wm_pos = use_wm ? (uint16_t *)ctx->buf("wm_pos", (size_t)sumnd * 2, &rc) : nullptr;   /* rank -> index */
         int32_t *wm_full = use_wm ? (int32_t *)ctx->buf("wm_full", (size_t)F * 4, &rc) : nullptr;
         if (rc != BPMX_OK) return rc;
@@ -451,12 +456,22 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
              * fixed overhead, worth paying only when CUs would sit idle */
             a.chunk = 8192;
             while (a.chunk > 1024 && (int64_t)F * ((maxnd + a.chunk - 1) / a.chunk) < 1024) a.chunk >>= 1;
+            /* the global-union kernel pays a window-sized fill per chunk: chunks of at least W */
+            if (merge_g) a.chunk = std::max<int64_t>(a.chunk, (W + RQ_T - 1) / RQ_T * RQ_T);
             const int64_t nch = (maxnd + a.chunk - 1) / a.chunk;
             if (nch > 65535) return fail(BPMX_E_LIMIT, "recording too long for the chunked rolling quantile");
             HIP_TRY(hipMemsetAsync(a.vfirst, 0x7F, (size_t)F * 4, s));      /* 0x7F7F7F7F: above any index */
             HIP_TRY(hipMemsetAsync(a.vlast, 0xFF, (size_t)F * 4, s));       /* -1 */
             const dim3 gq((unsigned)F, (unsigned)nch);
-            if (cap <= 16 * RQ_T) {
+            if (merge_g) {
+                a.gcap = gcap;
+                a.gv = (double *)ctx->buf("rollq_gv", (size_t)F * nch * 2 * gcap * 8, &rq_rc);
+                a.gp = (int32_t *)ctx->buf("rollq_gp", (size_t)F * nch * 2 * gcap * 4, &rq_rc);
+                if (rq_rc != BPMX_OK) return rq_rc;
+                (void)hipFuncSetAttribute((const void *)k_rolling_quantile_g<RQ_T>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g);
+                LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile_g<RQ_T>), gq, dim3(RQ_T), lds_g, s, a);
+            } else if (cap <= 16 * RQ_T) {
                 (void)hipFuncSetAttribute((const void *)k_rolling_quantile<RQ_T, 16>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 16>), gq, dim3(RQ_T), lds, s, a);

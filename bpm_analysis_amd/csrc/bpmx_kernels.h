@@ -99,6 +99,9 @@ struct RollqArgs {
     const int32_t *ntr;      /* ... when the file has <= WM_TRMAX of them (else read dense) */
     int64_t chunk;           /* k_rolling_quantile: outputs per workgroup (blockIdx.y = chunk of the file) */
     int32_t *vfirst, *vlast; /* [F] first / last valid output over all chunks (k_rollq_fill reads them) */
+    double *gv;              /* k_rolling_quantile_g: per-workgroup union scratch, 2 x gcap values ... */
+    int32_t *gp;             /* ... and 2 x gcap positions */
+    int64_t gcap;
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -175,6 +178,13 @@ __global__ void k_draft_bounds(DraftBoundArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);
+template <int T>
+__global__ void k_rolling_quantile_g(RollqArgs A);
+/* dynamic LDS of k_rolling_quantile_g<T> for a union capacity gcap */
+__host__ __device__ inline size_t rollq_g_lds_bytes(int T, int64_t gcap) {
+    return (size_t)T * 16 + (size_t)T * 8 + ((size_t)T + 1) * 4 + ((size_t)T / 64 + 2) * 4 + (size_t)T * 16 +
+           ((size_t)(gcap / 64) + 2) * 4;
+}
 __global__ void k_rollq_fill(RollqArgs A);
 
 /* wavelet-matrix rolling quantile (k_rollq_wm.hip): one 1024-thread workgroup

@@ -54,6 +54,7 @@ enum { TB_A = 0, TB_V = 0, TB_B = 16, TB_C = 20, TB_D = 24, TB_M = 25, TB_P = 41
  * blocks [[a, b], [-b, a]] — in its first 24 doubles; TT_VI = V^-1 */
 enum { TT_KPOW = 0, TT_MT = 96, TT_G0 = 112, TT_ALPHA = 128, TT_BETA = 384, TT_VI = 640, TT_SIZE = 656 };
 constexpr int NAT_PART = 16;          /* doubles per partial-tile block record: u4 v4 x pad3 S4 */
+constexpr int NAT_DSMAX = 1280;       /* decimation factors up to fs/300 - 1 at 384 kHz (tail buffers) */
 
 struct NatTile {
     int64_t s0;                         /* first frame of the tile (index into pcm frames) */
@@ -688,7 +689,7 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     /* what lane 0's sequential recursions read comes through LDS first: the
      * head's 16 samples, the tail's <= ds+1 samples (+16 for the mirror), the
      * partial tile's block records */
-    __shared__ double s_head[16], s_tail[320 + 20], s_ytl[320 + 20], s_part[64 * NAT_PART];
+    __shared__ double s_head[16], s_tail[NAT_DSMAX + 20], s_ytl[NAT_DSMAX + 20], s_part[64 * NAT_PART];
     const int64_t n = A.foff[f + 1] - A.foff[f];
     const int64_t fb = A.foff[f];
     const int64_t base = (nd - 1) * ds;                     /* x index of c_{nd-1} */
@@ -1279,7 +1280,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
                     const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active) {
     const int ds = P->ds;
-    if (ds > 300) return fail(BPMX_E_LIMIT, "native mode supports ds <= 300");
+    if (ds > NAT_DSMAX) return fail(BPMX_E_LIMIT, "native mode supports ds <= " + std::to_string(NAT_DSMAX));
     int rc = BPMX_OK;
     /* tables (cached on the host key; uploaded when they change) */
     /* tables and block offsets: rebuilt / re-uploaded only when they change (the

@@ -338,6 +338,253 @@ __global__ __launch_bounds__(T) void k_rolling_quantile(RollqArgs A) {
     }
 }
 
+/* The same sorted-union algorithm for windows beyond the LDS kernel (any
+ * noise_window_sec on any length): the union lives in global scratch, double
+ * buffered (a merge reads the old order and writes the new one, so no slice
+ * has to fit in registers), positions are absolute int32 (no 16-bit wrap),
+ * and the edge list carries (sorted index, relative position) as two words.
+ * Only the per-64-word edge prefix stays in LDS (cap/64 + 2 ints).  Each
+ * workgroup owns 2 x cap (f64 + i32) of scratch at A.gv / A.gp + wg * 2 cap. */
+template <int T>
+__global__ __launch_bounds__(T) void k_rolling_quantile_g(RollqArgs A) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files || !A.run[f]) return;
+    if (A.doff[f + 1] - A.doff[f] <= A.wm_max) return;       /* done by k_rollq_wm */
+    const int64_t c0 = (int64_t)blockIdx.y * A.chunk;
+    if (c0 >= A.doff[f + 1] - A.doff[f]) return;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int64_t cap = A.gcap;
+    const int64_t wg = (int64_t)blockIdx.x * gridDim.y + blockIdx.y;
+    double *Vb[2] = {A.gv + wg * 2 * cap, A.gv + wg * 2 * cap + cap};
+    int32_t *Pb[2] = {A.gp + wg * 2 * cap, A.gp + wg * 2 * cap + cap};
+    int cur = 0;
+    double *nsv = (double *)smem;                    /* [T] new values, sorted */
+    double *runv = nsv + T;                          /* [T] per-wave sorted runs */
+    int32_t *nsp = (int32_t *)(runv + T);            /* [T] */
+    int32_t *ubv = nsp + T;                          /* [T] */
+    int *rpref = ubv + T;                            /* [T+1] */
+    int *sh = rpref + T + 1;                         /* [T/64+2] */
+    int32_t *Ej = sh + T / 64 + 2;                   /* [2T] edge: sorted index */
+    int32_t *Er = Ej + 2 * T;                        /* [2T] edge: position relative to P0 */
+    int *wpre = Er + 2 * T;                          /* [cap/64 + 2] */
+    __shared__ int s_first, s_last, s_nE;
+
+    const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    const double *dense = A.dense + d0;
+    double *out = A.out + d0;
+    const int64_t W = A.window, minp = A.min_periods;
+    const int64_t t0 = A.troughs[d0];
+    const int64_t cend = c0 + A.chunk < n ? c0 + A.chunk : n;
+    const double q = A.q;
+    const double INF = __builtin_inf();
+    if (tid == 0) { s_first = INT_MAX; s_last = -1; }
+
+    int64_t nA = 0;
+    int64_t P0prev = 0, P1prev = 0;
+    for (int64_t i0 = c0; i0 < cend; i0 += T) {
+        const int64_t i1 = i0 + T < cend ? i0 + T : cend;
+        int64_t sA, eA, sB, eB;
+        win_bounds(i0, n, W, sA, eA);
+        win_bounds(i1 - 1, n, W, sB, eB);
+        const int64_t P0 = sA > t0 ? sA : t0;
+        const int64_t P1 = eB > P0 ? eB : P0;
+        bool pending_rem = false;
+        if (nA > 0 && P0 > P0prev) {
+            if (P0 >= P1prev) nA = 0;
+            else pending_rem = true;
+        }
+        int64_t a = P1prev > P0 ? P1prev : P0;
+        do {
+            const int64_t b = a + T < P1 ? a + T : P1;
+            const int nn = b > a ? (int)(b - a) : 0;
+            if (nn == 0 && !pending_rem) break;
+            const double *Av = Vb[cur];
+            const int32_t *Ap = Pb[cur];
+            double *Bv = Vb[cur ^ 1];
+            int32_t *Bp = Pb[cur ^ 1];
+            /* (1) this thread's slice of the old order: removed positions counted */
+            const int64_t CH = (nA + T - 1) / T;
+            const int64_t j0 = tid * CH < nA ? tid * CH : nA;
+            const int64_t j1 = j0 + CH < nA ? j0 + CH : nA;
+            int rc = 0;
+            if (pending_rem)
+                for (int64_t j = j0; j < j1; ++j) rc += Ap[j] < P0 ? 1 : 0;
+            /* (2) the new values: bitonic per wave, ranked across the runs */
+            double v = tid < nn ? dense[a + tid] : INF;
+            int p = tid;
+            for (int k = 2; k <= 64; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    const double vo = __shfl_xor(v, j);
+                    const int po = __shfl_xor(p, j);
+                    const bool other_less = vo < v || (vo == v && po < p);
+                    const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+                    if (lower == up ? other_less : !other_less) { v = vo; p = po; }
+                }
+            }
+            runv[tid] = v;
+            int rtot;
+            const int rpre = block_scan_int<T>(rc, sh, &rtot);
+            rpref[tid] = rpre;
+            if (tid == 0) rpref[T] = rtot;
+            int64_t ub = 0;
+            int r = lane;
+            if (p < nn) {
+                for (int w2 = 0; w2 < T / 64; ++w2) {
+                    if (w2 == wid) continue;
+                    const double *rv = runv + w2 * 64;
+                    int lo3 = 0, hi3 = 64;
+                    if (w2 < wid) {
+                        while (lo3 < hi3) { int mid = (lo3 + hi3) >> 1; if (rv[mid] <= v) lo3 = mid + 1; else hi3 = mid; }
+                    } else {
+                        while (lo3 < hi3) { int mid = (lo3 + hi3) >> 1; if (rv[mid] < v) lo3 = mid + 1; else hi3 = mid; }
+                    }
+                    r += lo3;
+                }
+                int64_t lo = 0, hi = nA;                 /* upper bound among the old values */
+                while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (Av[mid] <= v) lo = mid + 1; else hi = mid; }
+                ub = lo;
+                nsv[r] = v;
+                nsp[r] = (int32_t)(a + p);
+                ubv[r] = (int32_t)ub;
+            }
+            __syncthreads();
+            /* (3)+(4) old j -> j - removed_before(j) + #{new with ub <= j};
+             *         new rank r -> r + ub - removed_before(ub) */
+            {
+                int lo2 = 0, hi2 = nn;
+                while (lo2 < hi2) { int mid = (lo2 + hi2) >> 1; if (ubv[mid] <= j0) lo2 = mid + 1; else hi2 = mid; }
+                int ptr = lo2;
+                int64_t rm = rpre;
+                for (int64_t j = j0; j < j1; ++j) {
+                    while (ptr < nn && ubv[ptr] <= j) ptr++;
+                    const int32_t pj = Ap[j];
+                    if (pending_rem && pj < P0) { rm++; continue; }
+                    const int64_t dst = j - rm + ptr;
+                    Bv[dst] = Av[j];
+                    Bp[dst] = pj;
+                }
+            }
+            if (p < nn) {
+                int64_t rb = 0;
+                if (pending_rem) {
+                    const int64_t c = CH > 0 ? (ub / CH < T ? ub / CH : T) : 0;
+                    rb = rpref[c];
+                    for (int64_t j = c * CH; j < ub; ++j) rb += Ap[j] < P0 ? 1 : 0;
+                }
+                const int64_t dst = r + ub - rb;
+                Bv[dst] = v;
+                Bp[dst] = (int32_t)(a + p);
+            }
+            __syncthreads();
+            cur ^= 1;
+            nA = nA - rtot + nn;
+            pending_rem = false;
+            a = b;
+        } while (a < P1);
+        P0prev = P0;
+        P1prev = P1 > P1prev ? P1 : P1prev;
+        const double *Av = Vb[cur];
+        const int32_t *Ap = Pb[cur];
+
+        /* ---- edge list: sorted indices whose position may be outside some window of the tile ---- */
+        const int64_t LE = sB > t0 ? sB : t0, RE = eA;
+        const int nwords = (int)((nA + 63) >> 6);
+        for (int w = wid; w < nwords; w += T / 64) {
+            const int64_t j = ((int64_t)w << 6) + lane;
+            const int32_t pj = j < nA ? Ap[j] : 0;
+            const bool bit = j < nA && (pj < LE || pj >= RE);
+            const unsigned long long word = __ballot(bit);
+            if (lane == 0) wpre[w] = __popcll(word);
+        }
+        __syncthreads();
+        if (wid == 0) {                                  /* exclusive scan of the word counts */
+            int run = 0;
+            for (int w0 = 0; w0 < nwords; w0 += 64) {
+                const int c = w0 + lane < nwords ? wpre[w0 + lane] : 0;
+                int x = c;
+                for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(x, o); if (lane >= o) x += y; }
+                if (w0 + lane < nwords) wpre[w0 + lane] = run + x - c;
+                run += __shfl(x, 63);
+            }
+            if (lane == 0) s_nE = run;
+        }
+        __syncthreads();
+        for (int w = wid; w < nwords; w += T / 64) {
+            const int64_t j = ((int64_t)w << 6) + lane;
+            const int32_t pj = j < nA ? Ap[j] : 0;
+            const bool bit = j < nA && (pj < LE || pj >= RE);
+            const unsigned long long word = __ballot(bit);
+            if (bit) {
+                const int k = wpre[w] + __popcll(word & ((1ull << lane) - 1ull));
+                Ej[k] = (int32_t)j;
+                Er[k] = (int32_t)(pj - P0);
+            }
+        }
+        __syncthreads();
+        const int nE = s_nE;
+
+        /* ---- one output per thread (the LDS kernel's edge walk) ---- */
+        const int64_t i = i0 + tid;
+        int64_t s = 0, e = 0;
+        win_bounds(i < n ? i : n - 1, n, W, s, e);
+        const int64_t lo = s > t0 ? s : t0;
+        const int64_t nobs = (i < i1 && e > lo) ? e - lo : 0;
+        const bool valid = nobs >= minp && nobs > 0;
+        const int64_t xlo = lo - P0, xhi = e - P0;
+        int64_t k = 0;
+        double idxf = 0;
+        if (valid && nobs > 1) {
+            idxf = q * (double)(nobs - 1);
+            k = (int64_t)idxf;
+        }
+        int64_t jx = 0, m = 0;
+        if (valid) {
+            for (int u = 0; u < nE; ++u) {
+                const int64_t sj = Ej[u], pj = Er[u];
+                if (sj - jx > k) break;                  /* e_j - (j-1) never decreases */
+                const bool ex = pj < xlo || pj >= xhi;
+                m += ex ? 1 : 0;
+                jx += ex ? 1 : 0;
+            }
+        }
+        const int64_t qa = k + m;
+        int64_t qb = qa + 1;
+        if (valid && nobs > 1) {
+            for (;;) {
+                const int64_t rel = Ap[qb] - P0;
+                if (rel >= xlo && rel < xhi) break;
+                ++qb;
+            }
+        }
+        if (i < i1) {
+            double res = __builtin_nan("");
+            if (valid) {
+                const double va = Av[qa];
+                if (nobs == 1 || (double)k == idxf) res = va;
+                else {
+                    const double vb = Av[qb];
+                    res = va + (vb - va) * (idxf - (double)k);
+                }
+            }
+            out[i] = res;
+        }
+        {
+            const unsigned long long vm = __ballot(valid);
+            if (vm && lane == 0) {
+                atomicMin(&s_first, (int)(i0 + wid * 64 + __ffsll((long long)vm) - 1));
+                atomicMax(&s_last, (int)(i0 + wid * 64 + 63 - __clzll(vm)));
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && s_last >= 0) {
+        atomicMin(&A.vfirst[f], s_first);
+        atomicMax(&A.vlast[f], s_last);
+    }
+}
+template __global__ void k_rolling_quantile_g<256>(RollqArgs A);
+
 /* .bfill().ffill() of the chunked rolling quantile: nobs(i) is unimodal, so
  * the NaN outputs are a prefix and a suffix; fill them from the first and
  * last valid output over all chunks (or flag the recording all-NaN). */

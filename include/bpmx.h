@@ -82,8 +82,10 @@ enum bpmx_option {
                                     instead of deciding troughs from its bounds first (test/diagnostic) */
     BPMX_OPT_ROLLQ_NOPRUNE = 16, /* wavelet-matrix rolling quantile over every sample, without first dropping
                                     the samples no window's quantile can reach (test/diagnostic) */
-    BPMX_OPT_DRAFT_GLOBAL_RANK = 32 /* draft-floor bounds from the recording-wide segment order even for
+    BPMX_OPT_DRAFT_GLOBAL_RANK = 32, /* draft-floor bounds from the recording-wide segment order even for
                                        recordings of > 512 troughs (test/diagnostic; default ranks per window) */
+    BPMX_OPT_ROLLQ_GLOBAL = 64   /* force the global-memory sorted-union rolling quantile (test/diagnostic;
+                                    default: only for windows beyond the LDS kernel on long recordings) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

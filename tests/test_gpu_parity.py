@@ -288,11 +288,12 @@ def test_reference_side_ctypes_stub():
 
 @pytest.mark.parametrize("name", ["ref_44k_60s_mono", "ref_44k_40s_clicks", "ref_96k_20s_stereo"])
 def test_rolling_quantile_kernels_agree(det, name):
-    """The wavelet-matrix rolling quantile (default) and the sorted-union kernel
-    (BPMX_OPT_ROLLQ_MERGE) both reproduce the golden floor bit for bit."""
+    """The wavelet-matrix rolling quantile (default), the sorted-union kernel
+    (BPMX_OPT_ROLLQ_MERGE) and its global-memory form (BPMX_OPT_ROLLQ_GLOBAL)
+    all reproduce the golden floor bit for bit."""
     from bpm_analysis_amd import _native as N
     g = G.load(name)
-    for opt in (0, N.OPT_ROLLQ_MERGE):
+    for opt in (0, N.OPT_ROLLQ_MERGE, N.OPT_ROLLQ_GLOBAL):
         r = det.run_host([g["pcm"]], int(g["fs"]), g["params"], mode="reference", options=opt)[0]
         _check_file(r, g)
 
@@ -596,3 +597,36 @@ def test_native_batch_at_c3_scale(det):
         pk, env, fl, tr = h["peaks"], h["env"], h["floor"], h["troughs"]
         assert len(pk) > 100 and np.all(np.diff(pk) >= 15) and np.all(np.diff(tr) >= 15)
         assert np.all(env[pk] >= fl[pk]) and h["flags"] == 0
+
+
+@pytest.mark.parametrize("secs,window", [(600, 30.0), (180, 90.0), (75, 45.0)])
+def test_long_noise_window_on_long_recording(det, secs, window):
+    """noise_window_sec beyond the LDS kernels on recordings longer than the
+    wavelet-matrix limit (bpm_analysis.py:1083-1085 takes any window): the
+    global-memory sorted union, bit-exact against the oracle (reference mode)."""
+    params = dict(G.BASE_PARAMS, noise_window_sec=window)
+    pcm = O.synth(31337 + secs, 44100 * secs, 44100, 1)
+    r = det.run_host([pcm], 44100, params, mode="reference")[0]
+    o = O.detect(pcm, 44100, params, mode="reference")
+    _check_file(r, o)
+    assert len(r["peaks"]) > 50
+
+
+@pytest.mark.parametrize("fs,ds_param,ch", [(192000, 600, 1), (192000, 600, 2), (384000, 1270, 1)])
+def test_native_large_decimation(det, fs, ds_param, ch):
+    """Native mode beyond ds = 300 (a 192/384 kHz recording with downsample_factor
+    raised: bpm_analysis.py:1021-1029 accepts it up to fs/300 - 1) against the oracle."""
+    import torch
+    params = dict(G.BASE_PARAMS, downsample_factor=ds_param)
+    lens = [fs * 12 + 5, fs * 7]
+    recs = [O.synth(800 + i, n, fs, ch) for i, n in enumerate(lens)]
+    dev = torch.from_numpy(np.concatenate([r.reshape(-1) for r in recs])).to(det.device)
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    res = det.run(dev, fo, fs, params, mode="native", channels=ch, want_y=True)
+    torch.cuda.synchronize()
+    for h, pcm in zip(res.to_host(), recs):
+        o = O.detect(pcm, fs, params, mode="native")
+        assert h["sr"] == o["sr"] == fs // ds_param
+        scale = np.max(np.abs(o["y"]))
+        assert np.max(np.abs(h["y"] - o["y"])) <= 1e-9 * scale
+        _check_file(h, o, exact_env=False)
