@@ -646,6 +646,151 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
 template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 template __global__ void k_native_blocks_mfma<5>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 
+/* ---------------------------------------------------------------------- */
+/* int16 interleaved PCM (stereo; also mono beyond the matrix-core path's
+ * ds + 1 <= 160), f64 VALU block projections fed by LDS-DMA.
+ *
+ * At 96 kHz stereo a frame is 4 bytes and costs 8 f64 FMAs on the mean, so the
+ * VALU work (~1.7 ms per 30 GB of PCM chip-wide) sits below the HBM time: the
+ * kernel has to keep bytes in flight and the coefficients close.  Each wave
+ * owns one LDS slot (four waves per workgroup, one workgroup per CU) and walks
+ * the tile list: the slot is filled by global_load_lds_dwordx4 straight from
+ * HBM (no registers), and the next tile's DMA is issued as soon as the slot
+ * has been read, so it flies during this tile's epilogue and the other waves'
+ * work.  The (ds + 1) x 8 coefficient table lives in LDS too: at ds = 300 it
+ * is 19 KB, more than the scalar cache holds, and scalar loads that miss to L2
+ * serialise the wave (measured: 36 ms for a 30 GB C5 shard).  Two lanes share
+ * a block (lane b and b + 32: the first and second half of its frames), so a
+ * wave-uniform coefficient read (ds_read_b128 broadcast, one address per lane
+ * group) feeds up to 64 frame-block products; the halves are added with one
+ * lane exchange before the tile epilogue.
+ *
+ * Channel mean: sum_i c_i (L_i + R_i) / 2 is accumulated as sum_i c_i (L_i + R_i)
+ * and halved at the end — every partial sum differs by an exact factor of 2,
+ * so this equals accumulating c_i * ((L_i + R_i) / 2), the f64 mean the
+ * reference forms (bpm_analysis.py:1016). */
+constexpr int ND_WAVES = 4;
+constexpr int ND_LDS = 160 * 1024;
+
+/* host: DMA wave-instructions per tile (1 KiB each) so that four slots, the
+ * coefficient table and the epilogue constants fit the CU's LDS */
+inline int nd_ndma(int ds) {
+    const int coef = (ds + 1) * 64;
+    const int n = (ND_LDS - coef - 1024) / (ND_WAVES * 1024);
+    return n < 38 ? n : 38;
+}
+/* blocks per tile: the slot holds the <= 7-element alignment offset and
+ * (bt ds + 1) frames of ch int16 elements; at most 32 (two lanes per block) */
+inline int nd_tile_blocks(int ds, int ch) {
+    const int n = nd_ndma(ds);
+    if (n < 1) return 0;
+    const int b = ((n * 64 * 8 - 7) / ch - 1) / ds;
+    return b < 32 ? b : 32;
+}
+inline size_t nd_lds_bytes(int ds) { return (size_t)nd_ndma(ds) * ND_WAVES * 1024 + (size_t)(ds + 1) * 64 + ET_SIZE * 8; }
+
+template <int CH>
+__global__ __launch_bounds__(64 * ND_WAVES, 1) void k_native_blocks_dma(NatBlockArgs A, int ndma) {
+    typedef nat_u4 u4;
+    extern __shared__ __align__(16) unsigned char nd_smem[];
+    const int ds = A.ds, bt = A.bt;
+    const int slot_ch = ndma * 64;                        /* 16-byte chunks per slot */
+    u4 *slots = (u4 *)nd_smem;
+    double *s_coef = (double *)(slots + ND_WAVES * slot_ch);   /* [ds + 1][8] */
+    double *s_et = s_coef + (ds + 1) * 8;
+    nat_stage_epilogue_tables(A, s_et);
+    {
+        const double2 *src = (const double2 *)(A.tab + TB_COEF);
+        double2 *dst = (double2 *)s_coef;
+        for (int k = threadIdx.x; k < (ds + 1) * 4; k += blockDim.x) dst[k] = src[k];
+    }
+    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
+    const int16_t *pcm = (const int16_t *)A.pcm;
+    const int64_t total = A.total;                        /* int16 elements in the batch */
+    const int nch = (7 + (bt * ds + 1) * CH + 7) >> 3;    /* chunks a tile may touch (<= slot_ch) */
+    __syncthreads();                                      /* s_et, s_coef */
+    const int64_t clast = (total & ~(int64_t)7) - 8;
+    auto dma = [&](int64_t e0, u4 *slot) {
+        const int64_t a0 = e0 & ~(int64_t)7;
+        for (int r = 0; r < ndma; ++r) {
+            const int q = r * 64 + lane;
+            int64_t c = a0 + (int64_t)q * 8;
+            c = (q < nch && c + 8 <= total) ? c : clast;
+            const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(slot + r * 64);
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                         :: "v"(pcm + c), "s"(m0) : "memory");
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * ND_WAVES;
+    int64_t t = (int64_t)blockIdx.x * ND_WAVES + wv;
+    u4 *slot = slots + wv * slot_ch;
+    const int blk = lane & 31, hf = lane >> 5;
+    const int half = (ds + 2) >> 1;                       /* frames [0, half) | [half, ds] */
+    const int i0 = hf ? half : 0, i1 = hf ? ds + 1 : half;
+    NatTile tl{};
+    if (t < A.n_tiles) {
+        tl = nat_tile_ld(A.tiles, t);
+        dma(tl.s0 * CH, slot);
+    }
+    for (; t < A.n_tiles; t += stride) {
+        const int64_t tr = t + stride;
+        NatTile tn{};
+        if (tr < A.n_tiles) tn = nat_tile_ld(A.tiles, tr);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int64_t e0 = tl.s0 * CH;
+        const int coff = (int)(e0 & 7);                    /* elements before the tile's first frame */
+        {
+            const int64_t a0 = e0 - coff, tail0 = total & ~(int64_t)7;
+            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))   /* last tile of the batch */
+                ((int16_t *)slot)[tail0 - a0 + lane] = pcm[tail0 + lane];
+            __builtin_amdgcn_wave_barrier();
+        }
+        const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
+        double u0 = 0, u1 = 0, u2 = 0, u3 = 0, v0 = 0, v1 = 0, v2 = 0, v3 = 0, x0 = 0;
+        if (blk < Lt) {
+            auto acc = [&](double xv, int i) {
+                const double2 *c2 = (const double2 *)(s_coef + i * 8);
+                const double2 ca = c2[0], cb = c2[1], cc = c2[2], cd = c2[3];
+                u0 = __builtin_fma(ca.x, xv, u0); u1 = __builtin_fma(ca.y, xv, u1);
+                u2 = __builtin_fma(cb.x, xv, u2); u3 = __builtin_fma(cb.y, xv, u3);
+                v0 = __builtin_fma(cc.x, xv, v0); v1 = __builtin_fma(cc.y, xv, v1);
+                v2 = __builtin_fma(cd.x, xv, v2); v3 = __builtin_fma(cd.y, xv, v3);
+            };
+            if constexpr (CH == 2) {
+                const uint32_t *fr = (const uint32_t *)slot + (coff >> 1) + blk * ds;   /* one word per frame */
+                auto sum = [](uint32_t w) { return (double)((int)(int16_t)(w & 0xFFFFu) + ((int)w >> 16)); };
+                x0 = sum(fr[0]);
+                int i = i0;
+                for (; i + 4 <= i1; i += 4) {
+                    const uint32_t w0 = fr[i], w1 = fr[i + 1], w2 = fr[i + 2], w3 = fr[i + 3];
+                    acc(sum(w0), i); acc(sum(w1), i + 1); acc(sum(w2), i + 2); acc(sum(w3), i + 3);
+                }
+                for (; i < i1; ++i) acc(sum(fr[i]), i);
+            } else {
+                const int16_t *fr = (const int16_t *)slot + coff + blk * ds;
+                x0 = (double)fr[0];
+                int i = i0;
+                for (; i + 4 <= i1; i += 4) {
+                    const double a = fr[i], b = fr[i + 1], c = fr[i + 2], d = fr[i + 3];
+                    acc(a, i); acc(b, i + 1); acc(c, i + 2); acc(d, i + 3);
+                }
+                for (; i < i1; ++i) acc((double)fr[i], i);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the slot is read: refill it */
+        if (tr < A.n_tiles) dma(tn.s0 * CH, slot);
+        /* the second half's sums join the first (lane b += lane b + 32) */
+        u0 += __shfl_xor(u0, 32); u1 += __shfl_xor(u1, 32); u2 += __shfl_xor(u2, 32); u3 += __shfl_xor(u3, 32);
+        v0 += __shfl_xor(v0, 32); v1 += __shfl_xor(v1, 32); v2 += __shfl_xor(v2, 32); v3 += __shfl_xor(v3, 32);
+        if (CH == 2) { u0 *= 0.5; u1 *= 0.5; u2 *= 0.5; u3 *= 0.5; v0 *= 0.5; v1 *= 0.5; v2 *= 0.5; v3 *= 0.5; x0 *= 0.5; }
+        const bool valid = lane < Lt;
+        nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{u0, u1, u2, u3}, V4{v0, v1, v2, v3}, x0);
+        tl = tn;
+    }
+}
+template __global__ void k_native_blocks_dma<1>(NatBlockArgs, int);
+template __global__ void k_native_blocks_dma<2>(NatBlockArgs, int);
+
 /* One wave per recording:
  *   head  15 padded samples, exact sosfilt steps -> S at block 0 (lane 0);
  *   tiles S0_(t+1) = M^T S0_t + incl_t (forward carries, stored per tile):
@@ -1288,10 +1433,16 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* tiles of bt blocks: the int16 path's LDS tile holds <= NB_RCH*512 samples */
     /* matrix-core path: int16 mono, ds + 1 <= 160 (KS K steps of 32 samples) */
     const int mfma_ks = ds + 1 <= 96 ? 3 : (ds + 1 <= 160 ? 5 : 0);
-    const bool use_mfma = mfma_ks && P->dtype == BPMX_DT_I16 && P->channels == 1 && ((uintptr_t)B->pcm & 15) == 0 &&
+    const bool aligned16 = ((uintptr_t)B->pcm & 15) == 0;
+    const bool use_mfma = mfma_ks && P->dtype == BPMX_DT_I16 && P->channels == 1 && aligned16 &&
                           foff[F] >= 16 && !(P->options & BPMX_OPT_NATIVE_F64);
+    /* int16 stereo (and, on request, mono) through the LDS-DMA f64 kernel */
+    const bool use_dma = !use_mfma && P->dtype == BPMX_DT_I16 && aligned16 && foff[F] * P->channels >= 16 &&
+                         (P->channels == 2 || (P->channels == 1 && (P->options & BPMX_OPT_NATIVE_DMA))) &&
+                         !(P->options & BPMX_OPT_NATIVE_F64) && nd_tile_blocks(ds, P->channels) >= 1;
     /* tiles of bt blocks: the LDS tile (slot) must hold the tile's samples */
-    const int bt = use_mfma ? nm_tile_blocks(ds, mfma_ks) : std::min(64, (NB_RCH * 512 - 16) / ds);
+    const int bt = use_mfma ? nm_tile_blocks(ds, mfma_ks)
+                            : (use_dma ? nd_tile_blocks(ds, P->channels) : std::min(64, (NB_RCH * 512 - 16) / ds));
     std::vector<int64_t> key(16);
     for (int i = 0; i < 12; ++i) std::memcpy(&key[i], &P->sos[i], 8);
     key[12] = ds;
@@ -1383,6 +1534,20 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             else
                 LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma<5>, dim3(g1), dim3(64 * NM_WAVES), 0, s, a, af,
                        init, mt);
+        } else if (use_dma) {
+            a.total = foff[F] * P->channels;                 /* int16 elements */
+            const unsigned g1 = (unsigned)std::min<int64_t>((nt + ND_WAVES - 1) / ND_WAVES, 256);
+            const int ndma = nd_ndma(ds);
+            const size_t lds = nd_lds_bytes(ds);
+            if (P->channels == 2) {
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_dma<2>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_dma<2>, dim3(g1), dim3(64 * ND_WAVES), lds, s, a, ndma);
+            } else {
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_dma<1>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_dma<1>, dim3(g1), dim3(64 * ND_WAVES), lds, s, a, ndma);
+            }
         } else if (fast) {
             LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_i16, dim3(grid), dim3(64), 0, s, a,
                    (const double *)(d_tab + TB_COEF));

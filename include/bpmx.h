@@ -84,8 +84,10 @@ enum bpmx_option {
                                     the samples no window's quantile can reach (test/diagnostic) */
     BPMX_OPT_DRAFT_GLOBAL_RANK = 32, /* draft-floor bounds from the recording-wide segment order even for
                                        recordings of > 512 troughs (test/diagnostic; default ranks per window) */
-    BPMX_OPT_ROLLQ_GLOBAL = 64   /* force the global-memory sorted-union rolling quantile (test/diagnostic;
+    BPMX_OPT_ROLLQ_GLOBAL = 64,  /* force the global-memory sorted-union rolling quantile (test/diagnostic;
                                     default: only for windows beyond the LDS kernel on long recordings) */
+    BPMX_OPT_NATIVE_DMA = 128    /* native mode, int16 mono without the matrix-core path: the LDS-DMA f64
+                                    block kernel (default for int16 stereo) instead of the register-prefetch one */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

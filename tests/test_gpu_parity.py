@@ -630,3 +630,31 @@ def test_native_large_decimation(det, fs, ds_param, ch):
         scale = np.max(np.abs(o["y"]))
         assert np.max(np.abs(h["y"] - o["y"])) <= 1e-9 * scale
         _check_file(h, o, exact_env=False)
+
+
+@pytest.mark.parametrize("fs,ch,opt", [(96000, 2, 0), (48000, 2, 0), (44100, 2, 0), (96000, 1, 128)])
+def test_native_dma_block_kernel(det, fs, ch, opt):
+    """The LDS-DMA f64 block kernel (default for int16 stereo; BPMX_OPT_NATIVE_DMA
+    for mono) agrees with the f64 VALU kernels it replaces (BPMX_OPT_NATIVE_F64;
+    the stereo channel sum is halved once at the end, which is exact) and gives
+    the oracle's indices, on a ragged batch whose last recording ends on a
+    partial 16-byte chunk."""
+    import torch
+    from bpm_analysis_amd import _native as N
+    lens = [fs * 9 + 77, fs * 4, fs * 6 + 3]
+    recs = [O.synth(960 + i, n, fs, ch) for i, n in enumerate(lens)]
+    dev = torch.from_numpy(np.concatenate([r.reshape(-1) for r in recs])).to(det.device)
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    outs = []
+    for o in (opt, N.OPT_NATIVE_F64):
+        res = det.run(dev, fo, fs, params, mode="native", channels=ch, want_y=True, options=o)
+        torch.cuda.synchronize()
+        outs.append(res.to_host())
+    for a, b, pcm in zip(outs[0], outs[1], recs):
+        # the tile length differs between the kernels (64 vs fewer blocks), so the
+        # tile scans round differently: agreement to 1e-12 of the signal's scale
+        sy, se = np.max(np.abs(b["y"])), np.max(np.abs(b["env"]))
+        assert np.max(np.abs(a["y"] - b["y"])) <= 1e-12 * sy and np.max(np.abs(a["env"] - b["env"])) <= 1e-12 * se
+        o = O.detect(pcm, fs, params, mode="native")
+        _check_file(a, o, exact_env=False)
