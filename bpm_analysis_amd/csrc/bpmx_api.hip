@@ -335,6 +335,8 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     double *bmin = (double *)ctx->buf("bmin", (size_t)sumb * 8, &rc);
     double *qv = (double *)ctx->buf("qv", (size_t)F * Q_SLOTS * 8, &rc);
     int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
+    int32_t *vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
+    int32_t *fp_fb = (int32_t *)ctx->buf("fp_fallback", (size_t)F * 4, &rc);
     uint8_t *state = (uint8_t *)ctx->buf("state", (size_t)sumnd, &rc);
     if (rc != BPMX_OK) return rc;
     BlockStatArgs bs;
@@ -385,7 +387,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5;
-            LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+            a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
+            LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
+            a.only = fp_fb;                   /* recordings with more maxima than the LDS kernel holds */
+            LAUNCH(ctx, s, "k_find_peaks[troughs,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
         }
         if (bad_window)
             LAUNCH(ctx, s, "k_flag_window", k_flag_window, dim3((F + 255) / 256), dim3(256), 0, s, F, d_run1,
@@ -547,7 +552,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0;
-        LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+        a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
+        LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
+        a.only = fp_fb;
+        LAUNCH(ctx, s, "k_find_peaks[peaks,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
     }
     return BPMX_OK;
 }

@@ -69,6 +69,9 @@ struct PeakArgs {
     int32_t *nout;         /* [F] */
     int32_t *run_out;      /* optional [F]: 1 if nout >= run_min */
     int32_t run_min;
+    int32_t *vcand;        /* k_find_peaks_lds: scratch [sumNd], valley positions */
+    int32_t *fallback;     /* k_find_peaks_lds: [F] out, 1 = too many maxima for LDS (k_find_peaks takes it) */
+    const int32_t *only;   /* k_find_peaks: [F] or null, process only recordings with only[f] != 0 */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -172,6 +175,7 @@ __global__ void k_quantile(QuantArgs A);
 __global__ void k_quantile_reg(QuantArgs A, BlockStatArgs B);
 __global__ void k_block_stats(BlockStatArgs A);
 __global__ void k_find_peaks(PeakArgs A);
+__global__ void k_find_peaks_lds(PeakArgs A);
 __global__ void k_interp(InterpArgs A);
 __global__ void k_sanitize(SanitizeArgs A);
 __global__ void k_draft_bounds(DraftBoundArgs A);

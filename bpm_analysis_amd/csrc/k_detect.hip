@@ -380,7 +380,7 @@ constexpr int FP_MC = 2048;      /* candidates kept in LDS up to this many */
 
 __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f]) return;
+    if (f >= A.n_files || !A.active[f] || (A.only && !A.only[f])) return;
     const int64_t d0 = A.doff[f];
     const int64_t n = A.doff[f + 1] - d0;
     const double *e = A.env + d0;
@@ -593,6 +593,223 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
         if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
     }
     STAMP(4);
+    STAMP_FLUSH(A.stamps);
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_find_peaks_lds: the same find_peaks, with prominences from the local
+ * extrema held in LDS instead of walks over the samples in global memory.
+ *
+ * Between two consecutive local maxima c_i, c_(i+1) of the signal (scipy's
+ * _local_maxima_1d, plateau midpoints) there is no other local maximum, so
+ * the samples there fall to exactly one valley (a strict local minimum or a
+ * flat bottom) and rise again; call its value v_i.  v_(-1) = min(x[0], the
+ * valley before c_0, if any) and v_(M-1) = min(x[n-1], the valley after the
+ * last maximum) cover the edges.  _peak_prominences (wlen = -1) walks left
+ * from peak c_j while x <= x[c_j] and stops at the first higher sample; every
+ * sample it passes lies in gaps k* .. j-1, where c_k* is the nearest maximum
+ * with x[c_k*] > x[c_j] (the higher sample sits on c_k*'s falling slope), and
+ * each gap's minimum is its valley, so
+ *     left_min = min(v_k*, ..., v_(j-1))   (k* = -1 if none is higher)
+ * and symmetrically on the right.  All of it is in LDS: per recording ~1000
+ * maxima (native mode) to ~2400 (reference mode); a recording with more than
+ * FL_MC maxima is flagged for k_find_peaks.  Everything else — height,
+ * distance rounds, prominence threshold, ordered output — is k_find_peaks'. */
+constexpr int FL_MC = 3072;
+
+__global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files) return;
+    const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+    if (!A.active[f]) {
+        if (tid == 0) A.fallback[f] = 0;
+        return;
+    }
+    const int64_t d0 = A.doff[f];
+    const int64_t n = A.doff[f + 1] - d0;
+    const double *e = A.env + d0;
+    const double *h = A.height ? A.height + d0 : nullptr;
+    const double sg = A.sign;
+    const double INF = __builtin_inf();
+    constexpr int NW = FP_T / 64;
+    constexpr int FP_G = 4;                                  /* iterations per load group (register budget) */
+    __shared__ int32_t s_mp[FL_MC];
+    __shared__ double s_mh[FL_MC];
+    __shared__ double s_vv[FL_MC + 1];
+    __shared__ uint8_t s_st[FL_MC];
+    __shared__ double s_bh[FL_MC / 32], s_bvl[FL_MC / 32], s_bvr[FL_MC / 32];
+    __shared__ int s_gc[2][FP_G][NW];
+    __shared__ int sh[NW + 1];
+    __shared__ int s_flag;
+    STAMP_DECL
+
+    /* (1) local maxima (plateau midpoints) and valley starts, in order: wave w
+     * scans its own contiguous run of positions 64 at a time (coalesced loads,
+     * no workgroup barrier), compacting its hits into its own stretch of the
+     * global scratch (a run of c positions holds at most c hits); one scan of
+     * the 16 per-wave counts then places every run */
+    const int64_t span = n > 2 ? n - 2 : 0;                  /* positions 1 .. n-2 */
+    const int64_t chunk = ((span + NW - 1) / NW + 63) & ~(int64_t)63;
+    const int64_t w0 = 1 + (int64_t)wid * chunk, w1 = min<int64_t>(n - 1, w0 + chunk);
+    int32_t *mp_g = A.cand + d0, *vp_g = A.vcand + d0;
+    int cm = 0, cv = 0;                                      /* wave-uniform counts */
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int64_t b = w0; b < w1; b += 64) {
+        const int64_t i = b + lane;
+        bool ism = false, isv = false;
+        int32_t pk = 0;
+        if (i < w1) {
+            const double xi = sg * e[i], xl = sg * e[i - 1];
+            if (xl != xi) {
+                int64_t ia = i + 1;
+                while (ia < n - 1 && sg * e[ia] == xi) ia++;
+                const double xr = sg * e[ia];
+                if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
+                else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)i; }
+            }
+        }
+        const unsigned long long bm = __ballot(ism), bv = __ballot(isv);
+        if (ism) mp_g[w0 - 1 + cm + __popcll(bm & lt)] = pk;
+        if (isv) vp_g[w0 - 1 + cv + __popcll(bv & lt)] = pk;
+        cm += __popcll(bm);
+        cv += __popcll(bv);
+    }
+    if (lane == 0) { s_gc[0][0][wid] = cm; s_gc[1][0][wid] = cv; }
+    __syncthreads();
+    int M = 0, om = 0;
+    for (int w = 0; w < NW; ++w) {
+        if (w == wid) om = M;
+        M += s_gc[0][0][w];
+    }
+    STAMP(1);
+    if (M > FL_MC) {                                         /* k_find_peaks takes this recording */
+        if (tid == 0) A.fallback[f] = 1;
+        return;
+    }
+    if (tid == 0) A.fallback[f] = 0;
+    const int64_t dist = A.distance;
+    for (int t = lane; t < cm; t += 64) {                    /* this wave's run of maxima */
+        const int32_t p = mp_g[w0 - 1 + t];
+        const double xv = sg * e[p];
+        const int k = om + t;
+        s_mp[k] = p;
+        s_mh[k] = xv;
+        s_st[k] = (!h || h[p] <= xv) ? (dist > 1 ? ST_UNDECIDED : ST_KEPT) : ST_REMOVED;   /* height filter */
+    }
+    for (int k = tid; k <= M; k += FP_T) s_vv[k] = k == 0 ? sg * e[0] : (k == M ? sg * e[n - 1] : INF);
+    __syncthreads();
+    /* valley -> its gap: gap g (between c_g and c_(g+1)) is s_vv[g + 1] */
+    for (int t = lane; t < cv; t += 64) {
+        const int32_t pv = vp_g[w0 - 1 + t];
+        int lo = 0, hi = M;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_mp[mid] < pv) lo = mid + 1; else hi = mid; }
+        const double val = sg * e[pv];
+        if (lo == 0 || lo == M) s_vv[lo] = fmin(s_vv[lo], val);   /* edge gaps: at most one valley each */
+        else s_vv[lo] = val;
+    }
+    __syncthreads();
+    STAMP(2);
+
+    /* (3) distance: rounds of local decisions (k_find_peaks' rule) */
+    if (dist > 1) {
+        for (int round = 0; round <= M; ++round) {
+            if (tid == 0) s_flag = 0;
+            __syncthreads();
+            bool pending = false;
+            for (int j = tid; j < M; j += FP_T) {
+                if (ld_state(&s_st[j]) != ST_UNDECIDED) continue;
+                const int64_t pj = s_mp[j];
+                const double vj = s_mh[j];
+                bool killed = false, blocked = false;
+                for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
+                    if (s_mh[k] > vj) {
+                        const uint8_t st = ld_state(&s_st[k]);
+                        if (st == ST_KEPT) { killed = true; break; }
+                        if (st == ST_UNDECIDED) blocked = true;
+                    }
+                }
+                if (!killed) {
+                    for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k) {
+                        if (s_mh[k] >= vj) {
+                            const uint8_t st = ld_state(&s_st[k]);
+                            if (st == ST_KEPT) { killed = true; break; }
+                            if (st == ST_UNDECIDED) blocked = true;
+                        }
+                    }
+                }
+                if (killed) st_state(&s_st[j], ST_REMOVED);
+                else if (!blocked) st_state(&s_st[j], ST_KEPT);
+                else pending = true;
+            }
+            if (pending) s_flag = 1;
+            __syncthreads();
+            const int again = s_flag;
+            __syncthreads();
+            if (!again) break;
+        }
+    }
+    STAMP(3);
+
+    /* (4) prominences of the kept maxima, one thread each: walk the maxima
+     * outwards to the nearest higher one, taking the gap valleys passed on the
+     * way; runs of 32 maxima that are all no higher are skipped whole through
+     * their block maximum and block valley minimum */
+    {
+        const int NB32 = (M + 31) >> 5;
+        for (int b = tid; b < NB32; b += FP_T) {
+            double hx = -INF, vl = INF, vr = INF;
+            for (int k = b * 32; k < min(M, b * 32 + 32); ++k) {
+                hx = fmax(hx, s_mh[k]);
+                vl = fmin(vl, s_vv[k + 1]);                  /* gaps k (left walks)       */
+                vr = fmin(vr, s_vv[k]);                      /* gaps k - 1 (right walks) */
+            }
+            s_bh[b] = hx;
+            s_bvl[b] = vl;
+            s_bvr[b] = vr;
+        }
+        __syncthreads();
+        const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
+        for (int j = tid; j < M; j += FP_T) {
+            if (s_st[j] != ST_KEPT) continue;
+            const double hj = s_mh[j];
+            double lmin = INF, rmin = INF;
+            for (int k = j - 1;;) {
+                if (k < 0) { lmin = fmin(lmin, s_vv[0]); break; }
+                if ((k & 31) == 31 && s_bh[k >> 5] <= hj) { lmin = fmin(lmin, s_bvl[k >> 5]); k -= 32; continue; }
+                lmin = fmin(lmin, s_vv[k + 1]);
+                if (s_mh[k] > hj) break;
+                --k;
+            }
+            for (int k = j + 1;;) {
+                if (k >= M) { rmin = fmin(rmin, s_vv[M]); break; }
+                if ((k & 31) == 0 && k + 31 < M && s_bh[k >> 5] <= hj) { rmin = fmin(rmin, s_bvr[k >> 5]); k += 32; continue; }
+                rmin = fmin(rmin, s_vv[k]);
+                if (s_mh[k] > hj) break;
+                ++k;
+            }
+            const double prom = hj - fmax(lmin, rmin);
+            st_state(&s_st[j], thr <= prom ? ST_FINAL : ST_REMOVED);
+        }
+    }
+    __syncthreads();
+    STAMP(4);
+
+    /* (5) ordered compaction */
+    int64_t *out = A.out + d0;
+    int w = 0;
+    for (int q0 = 0; q0 < M; q0 += FP_T) {
+        const int j = q0 + tid;
+        const bool keep = j < M && s_st[j] == ST_FINAL;
+        int tot;
+        const int off = block_scan_flag<FP_T>(keep, sh, &tot);
+        if (keep) out[w + off] = s_mp[j];
+        w += tot;
+    }
+    if (tid == 0) {
+        A.nout[f] = w;
+        if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
+    }
+    STAMP(5);
     STAMP_FLUSH(A.stamps);
 }
 

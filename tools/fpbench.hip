@@ -49,6 +49,9 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&d_nout, F * 4));
     CK(hipMalloc(&d_state, env.size()));
     CK(hipMalloc(&d_st, (size_t)F * 16 * 8));
+    int32_t *d_vc, *d_fb;
+    CK(hipMalloc(&d_vc, env.size() * 4));
+    CK(hipMalloc(&d_fb, F * 4));
     CK(hipMemcpy(d_env, env.data(), env.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_qv, qv.data(), qv.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_doff, doff.data(), (F + 1) * 8, hipMemcpyHostToDevice));
@@ -62,14 +65,17 @@ int main(int argc, char **argv) {
         a.env = d_env; a.height = nullptr; a.doff = d_doff; a.boff = d_boff; a.active = d_act; a.bmax = d_bmx;
         a.bmin = d_bmn; a.qv = d_qv; a.qslot = sg < 0 ? Q_TROUGH : Q_PEAK; a.n_files = (int)F; a.distance = 15;
         a.sign = sg; a.cand = d_cand; a.state = d_state; a.out = d_out; a.nout = d_nout; a.run_out = nullptr;
-        a.run_min = 0; a.stamps = d_st;
+        a.run_min = 0; a.stamps = d_st; a.vcand = d_vc; a.fallback = d_fb; a.only = nullptr;
+        const bool lds = argc > 2 && argv[2][0] == 'l';
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         float best = 1e9;
         for (int rep = 0; rep < 5; ++rep) {
             CK(hipEventRecord(e0, 0));
-            hipLaunchKernelGGL(k_find_peaks, dim3(F), dim3(FP_T), 0, 0, a);
+            CK(hipMemset(d_st, 0, (size_t)F * 16 * 8));
+            if (lds) hipLaunchKernelGGL(k_find_peaks_lds, dim3(F), dim3(FP_T), 0, 0, a);
+            else hipLaunchKernelGGL(k_find_peaks, dim3(F), dim3(FP_T), 0, 0, a);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -86,7 +92,9 @@ int main(int argc, char **argv) {
         for (int k = 0; k < 8; ++k) tot += sum[k];
         long long np = 0;
         for (auto v : no) np += v;
-        const char *names[8] = {"tables", "maxima", "distance", "prominence", "compact", "(prom max wave)", "(prom mean wave)", "-"};
+        const char *names0[8] = {"tables", "maxima", "distance", "prominence", "compact", "(prom max wave)", "(prom mean wave)", "-"};
+        const char *names1[8] = {"-", "extrema", "to LDS", "distance", "prominence", "compact", "-", "-"};
+        const char **names = lds ? names1 : names0;
         printf("sign %+.0f: %.3f ms, %lld peaks; per-WG cycles %.0f\n", sg, best, np, tot / F);
         for (int k = 0; k < 8; ++k)
             if (sum[k] > 0) printf("   %-11s %10.0f  %5.1f%%\n", names[k], sum[k] / F, 100 * sum[k] / tot);
