@@ -370,7 +370,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         }
         a.n_levels = L;
         a.skip = nullptr;
-        a.stats = 1;
+        a.stats = 0;                      /* k_find_peaks builds its own block tables when it runs */
         LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
         if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(1024), 0, s, a);
     }

@@ -395,11 +395,19 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     __shared__ uint8_t s_st[FP_MC];
     STAMP_DECL
 
-    /* block tables into LDS (the prominence walks read them) */
+    /* block tables (the prominence walks read them): computed here into LDS
+     * for recordings they fit (this kernel only runs for the few recordings
+     * k_find_peaks_lds hands over), from k_block_stats' global tables beyond */
     const int64_t nblk = (n + 63) >> 6;
     const double *bmx = A.bmax + A.boff[f], *bmn = A.bmin + A.boff[f];
     if (nblk <= FP_NBMAX) {
-        for (int64_t b = tid; b < nblk; b += FP_T) { s_bmx[b] = bmx[b]; s_bmn[b] = bmn[b]; }
+        const double INF = __builtin_inf();
+        for (int64_t b = wave_id(); b < nblk; b += FP_T / 64) {
+            const int64_t i = (b << 6) + lane_id();
+            const double v = i < n ? e[i] : 0.0;
+            const double mx = wave_max(i < n ? v : -INF), mn = wave_min(i < n ? v : INF);
+            if (lane_id() == 0) { s_bmx[b] = mx; s_bmn[b] = mn; }
+        }
         bmx = s_bmx;
         bmn = s_bmn;
     }

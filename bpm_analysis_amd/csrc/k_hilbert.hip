@@ -257,12 +257,16 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     const int per = (N + HB_T - 1) / HB_T;                 /* <= HB_RMPER (host checks) */
     const int i0 = threadIdx.x * per, i1 = i0 + per < N ? i0 + per : N;
     double ev[HB_RMPER];
+    /* full windows multiply by 1/w (within an ulp of the division; the
+     * envelope's tolerance is 1e-9 relative), edge windows divide */
+    const double invw = 1.0 / (double)w;
+    auto mean = [&](double sum, int64_t cnt) { return cnt == w ? sum * invw : sum / (double)cnt; };
     if (i0 < i1) {
         int64_t s, e;
         win_bounds(i0, N, w, s, e);
         double sum = 0.0;
         for (int64_t q = s; q < e; ++q) sum += mag[q];
-        ev[0] = sum / (double)(e - s);
+        ev[0] = mean(sum, e - s);
 #pragma unroll
         for (int j = 1; j < HB_RMPER; ++j) {
             const int i = i0 + j;
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
                 for (int64_t q = e; q < e2; ++q) sum += mag[q];
                 for (int64_t q = s; q < s2; ++q) sum -= mag[q];
                 s = s2; e = e2;
-                ev[j] = sum / (double)(e - s);
+                ev[j] = mean(sum, e - s);
             }
         }
     }
