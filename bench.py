@@ -522,16 +522,30 @@ def main():
     host_beats = None
     if args.host_beat_files > 0:
         from bpm_analysis_amd import beats
-        res = gpu_host[:args.host_beat_files]
+        # native stages (libbpmx_host.so) on every file of the batch, over the
+        # rank's host threads: their beats and BPM curves go into the gather
+        hth = max(1, cpu_threads()[0] // int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         th0 = time.perf_counter()
-        done = beats.analyze_many(res, params)
-        hdt = time.perf_counter() - th0
-        for f, a in enumerate(done):
+        fast = beats.analyze_fast(gpu_host, params, threads=hth)
+        ndt = time.perf_counter() - th0
+        for f, a in enumerate(fast):
             if "error" not in a:
-                rows[f] = FileResult.from_analysis(rank * F + f, res[f]["peaks"], res[f]["flags"], a)
-        host_beats = {"files": len(res), "cores": 1, "files_per_s": len(res) / hdt,
-                      "audio_samples_per_s": len(res) * n / hdt, "ms_per_file": hdt / len(res) * 1e3,
-                      "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))}
+                rows[f] = FileResult(rank * F + f, gpu_host[f]["peaks"], a["final_peaks"], a["bpm_times"], a["bpm"],
+                                     gpu_host[f]["flags"])
+        # the Python stages (beats.py: also HRV, slopes, debug strings) on a sample, one core
+        res = gpu_host[:args.host_beat_files]
+        th1 = time.perf_counter()
+        done = beats.analyze_many(res, params)
+        hdt = time.perf_counter() - th1
+        same = all(np.array_equal(d["final_peaks"], a["final_peaks"]) for d, a in zip(done, fast)
+                   if "error" not in d and "error" not in a)
+        host_beats = {"native": {"files": F, "threads": hth, "files_per_s": F / ndt, "ms_per_file_per_thread":
+                                 ndt / F * hth * 1e3, "wall_ms": ndt * 1e3,
+                                 "final_beats": int(sum(len(a["final_peaks"]) for a in fast if "error" not in a))},
+                      "python": {"files": len(res), "cores": 1, "files_per_s": len(res) / hdt,
+                                 "ms_per_file": hdt / len(res) * 1e3,
+                                 "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))},
+                      "native_equals_python": bool(same)}
     tg0 = time.perf_counter()
     allres = gather_file_results(rows, world * F, device=det.device if world > 1 else None)
     gathered = None

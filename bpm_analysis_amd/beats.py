@@ -703,3 +703,28 @@ def analyze_many(results: Sequence[Dict], params: Dict, start_bpm_hint: Optional
     chunk = max(1, len(jobs) // (4 * workers))
     with ProcessPoolExecutor(max_workers=workers, mp_context=multiprocessing.get_context("spawn")) as ex:
         return list(ex.map(_analyze_one, jobs, chunksize=chunk))
+
+
+def analyze_fast(results: Sequence[Dict], params: Dict, start_bpm_hint: Optional[float] = None,
+                 threads: int = 1) -> List[Dict]:
+    """The beat stages the batch path needs — preliminary pass, classifier,
+    refinement and the smoothed BPM curve — as native code (libbpmx_host.so,
+    include/bpmx_host.h) over the per-file dicts of a batched GPU run, on
+    ``threads`` host threads (the C++ releases the GIL).  Per file:
+    dict(final_peaks, bpm_times, bpm, start_bpm, peak_time, recovery_time,
+    tags), or the entry's / the stage's ``error``.  The same beats and curve
+    as ``analyze_recording`` (tests/test_host_beats.py); HRV, slopes, reports
+    and the plot stay with analyze_recording."""
+    from . import _host
+    bp = _host.beat_params(params)
+
+    def one(r):
+        if "error" in r:
+            return r
+        return _host.beats(r["env"], r["sr"], r["floor"], r["peaks"], bp, start_bpm_hint)
+
+    if threads <= 1 or len(results) < 2:
+        return [one(r) for r in results]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(one, results))

@@ -117,8 +117,8 @@ def _pad_rows(rows: List[np.ndarray], width: int, fill, dtype) -> np.ndarray:
 
 
 def run_sharded(items: Sequence, params: dict, fs: Optional[int] = None, mode: str = "native",
-                start_bpm_hint: Optional[float] = None, beats: bool = True, detector=None,
-                group=None) -> Optional[List[dict]]:
+                start_bpm_hint: Optional[float] = None, beats="native", detector=None,
+                group=None, host_threads: int = 0, chunk_frames: int = 1 << 30) -> Optional[List[dict]]:
     """A ragged batch of independent recordings over the ranks of a
     torch.distributed process group (one process per GPU); the
     per-file loop it replaces is gui.py:202-251.
@@ -128,8 +128,11 @@ def run_sharded(items: Sequence, params: dict, fs: Optional[int] = None, mode: s
     * Placement: ``lpt_partition`` of the frame counts; every rank derives it
       from the same lengths, so no plan is exchanged.
     * Per rank: the hot path on its GPU (``detector``: an engine.Detector; one
-      ragged batch per rate/format/channel group), then the host beat stages
-      (beats.analyze_recording: classifier, refinement, smoothed BPM curve).
+      ragged batch per rate/format/channel group, cut into chunks of about
+      ``chunk_frames`` frames), and the host beat stages of each chunk on
+      ``host_threads`` host threads while the GPU runs the next chunk
+      (``beats="native"``: libbpmx_host.so, beats.analyze_fast;
+      ``"python"``: beats.analyze_recording; False: raw peaks only).
     * Result gather to rank 0 (RCCL under the "nccl" backend, gloo on CPU):
       one int64 slab [files, 4 + raw peaks + final beats] and one f64 slab
       [files, 2 x BPM-curve points] per rank, padded to the widest over all
@@ -148,25 +151,63 @@ def run_sharded(items: Sequence, params: dict, fs: Optional[int] = None, mode: s
         detector = Detector(int(os.environ.get("LOCAL_RANK", "0")))
     lengths = _lengths(items)
     mine = lpt_partition(lengths, world)[rank]
-    det_res = _detect_local(items, mine, fs, params, mode, detector)
-
-    rows = []
-    for i in mine:
-        r = det_res[i]
-        if "error" in r:
-            rows.append(FileResult(i, error=r["error"]))
-            continue
-        pk = np.asarray(r["peaks"], dtype=np.int64)
-        if not beats:
-            rows.append(FileResult(i, raw_peaks=pk, flags=int(r["flags"])))
-            continue
-        from .beats import analyze_recording
+    if host_threads <= 0:
         try:
-            a = analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], pk, params, start_bpm_hint)
-        except Exception as exc:                       # per file, as the GUI loop catches it (gui.py:247-251)
-            rows.append(FileResult(i, error=exc))
-            continue
-        rows.append(FileResult.from_analysis(i, pk, int(r["flags"]), a))
+            host_threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        except AttributeError:
+            host_threads = 1
+    chunks, cur, acc = [], [], 0                       # longest first (LPT order), ~chunk_frames each
+    for i in mine:
+        cur.append(i)
+        acc += lengths[i]
+        if acc >= chunk_frames:
+            chunks.append(cur)
+            cur, acc = [], 0
+    if cur:
+        chunks.append(cur)
+
+    def host_stage(idx, det_res):
+        out = []
+        for i in idx:
+            r = det_res[i]
+            if "error" in r:
+                out.append(FileResult(i, error=r["error"]))
+                continue
+            pk = np.asarray(r["peaks"], dtype=np.int64)
+            if not beats:
+                out.append(FileResult(i, raw_peaks=pk, flags=int(r["flags"])))
+                continue
+            if beats == "python":
+                from .beats import analyze_recording
+                try:
+                    a = analyze_recording(r["env"], r["sr"], r["floor"], r["troughs"], pk, params, start_bpm_hint)
+                except Exception as exc:               # per file, as the GUI loop catches it (gui.py:247-251)
+                    out.append(FileResult(i, error=exc))
+                    continue
+                out.append(FileResult.from_analysis(i, pk, int(r["flags"]), a))
+                continue
+            from . import _host
+            a = _host.beats(r["env"], r["sr"], r["floor"], pk, bparams, start_bpm_hint)
+            if "error" in a:
+                out.append(FileResult(i, error=a["error"]))
+            else:
+                out.append(FileResult(i, pk, a["final_peaks"], a["bpm_times"], a["bpm"], int(r["flags"])))
+        return out
+
+    bparams = None
+    if beats and beats != "python":
+        from . import _host
+        bparams = _host.beat_params(params)
+    from concurrent.futures import ThreadPoolExecutor
+    rows: List[FileResult] = []
+    with ThreadPoolExecutor(host_threads) as ex:
+        futs = []
+        for idx in chunks:                             # the GPU runs chunk k+1 while host threads take chunk k
+            det_res = _detect_local(items, idx, fs, params, mode, detector)
+            per = max(1, len(idx) // host_threads)
+            futs += [ex.submit(host_stage, idx[a:a + per], det_res) for a in range(0, len(idx), per)]
+        for fu in futs:
+            rows += fu.result()
     dev = detector.device if (dist.is_initialized() and dist.get_backend(group) == "nccl") else None
     return gather_file_results(rows, len(items), group=group, device=dev)
 

@@ -133,29 +133,32 @@ def _sharded_items():
     return [O.synth(40 + i, n, 44100, 1) for i, n in enumerate(lens)]
 
 
-def _sharded_worker(rank, world, port, q):
+def _sharded_worker(rank, world, port, q, beats):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from bpm_analysis_amd import DEFAULT_PARAMS
     from bpm_analysis_amd.shard import lpt_partition, run_sharded
     items = _sharded_items()
     params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
-    res = run_sharded(items, params, fs=44100, mode="native", detector=_OracleDetector())
+    res = run_sharded(items, params, fs=44100, mode="native", detector=_OracleDetector(), beats=beats,
+                      host_threads=2, chunk_frames=44100 * 30)     # several GPU chunks per rank
     q.put((rank, res, lpt_partition([len(x) for x in items], world)))
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_runner_gathers_peaks_and_bpm_curves():
-    """shard.run_sharded over 2 gloo ranks: LPT placement, per-rank detection
-    and host beat stages, and the rank-0 gather of raw peaks, final beats and
-    the smoothed BPM curve, equal to the single-process result file by file."""
+@pytest.mark.parametrize("stages", ["native", "python"])
+def test_two_rank_sharded_runner_gathers_peaks_and_bpm_curves(stages):
+    """shard.run_sharded over 2 gloo ranks: LPT placement, per-rank detection in
+    chunks with the host beat stages (native C++ or Python) on host threads,
+    and the rank-0 gather of raw peaks, final beats and the smoothed BPM
+    curve, equal to the single-process result file by file."""
     import numpy as np
     from bpm_analysis_amd import DEFAULT_PARAMS, beats
     from oracle import oracle as O
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, stages)) for r in range(world)]
     for p in ps:
         p.start()
     outs = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x[0])

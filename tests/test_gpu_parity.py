@@ -658,3 +658,28 @@ def test_native_dma_block_kernel(det, fs, ch, opt):
         assert np.max(np.abs(a["y"] - b["y"])) <= 1e-12 * sy and np.max(np.abs(a["env"] - b["env"])) <= 1e-12 * se
         o = O.detect(pcm, fs, params, mode="native")
         _check_file(a, o, exact_env=False)
+
+
+def test_run_sharded_single_rank_on_the_gpu(det, tmp_path):
+    """shard.run_sharded with the GPU detector (one rank, no process group):
+    WAV paths of mixed rates in chunks, native beat stages on host threads;
+    raw peaks bit-exact against the oracle, beats and BPM curve equal to the
+    Python stages on the same outputs."""
+    from scipy.io import wavfile
+    from bpm_analysis_amd import beats as B
+    from bpm_analysis_amd import DEFAULT_PARAMS
+    from bpm_analysis_amd.shard import run_sharded
+    params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
+    specs = [(44100, 44100 * 40, 1), (48000, 48000 * 25, 2), (44100, 44100 * 33 + 7, 1), (96000, 96000 * 20, 2)]
+    paths = []
+    for i, (fs, n, ch) in enumerate(specs):
+        paths.append(str(tmp_path / f"r{i}.wav"))
+        wavfile.write(paths[-1], fs, O.synth(60 + i, n, fs, ch))
+    res = run_sharded(paths, params, mode="native", detector=det, host_threads=2, chunk_frames=44100 * 50)
+    for (fs, n, ch), path, r in zip(specs, paths, res):
+        pcm = wavfile.read(path)[1]
+        o = O.detect(pcm, fs, params, mode="native")
+        assert _same(r["raw_peaks"], o["peaks"])
+        a = B.analyze_recording(o["env"], o["sr"], o["floor"], o["troughs"], o["peaks"], params)
+        assert _same(r["final_peaks"], a["final_peaks"])
+        np.testing.assert_allclose(r["bpm"], a["final_metrics"]["smoothed_bpm"].values, rtol=1e-12, atol=0)
