@@ -61,6 +61,9 @@ def load() -> ctypes.CDLL:
     P = ctypes.c_void_p
     L.bpmx_beats.argtypes = [P, _I, P, P, _I, ctypes.c_int32, ctypes.POINTER(BeatParams), _D, P, P, P, P, P, P, P]
     L.bpmx_beats.restype = ctypes.c_int
+    L.bpmx_beats_batch.argtypes = [ctypes.c_int32, P, P, P, P, P, P, ctypes.POINTER(BeatParams), _D, ctypes.c_int32,
+                                   P, P, P, P, P, P, P, P]
+    L.bpmx_beats_batch.restype = ctypes.c_int
     if L.bpmx_host_abi_version() != ABI_VERSION:
         raise RuntimeError("libbpmx_host ABI mismatch; rebuild")
     _lib = L
@@ -95,3 +98,52 @@ def beats(env: np.ndarray, sr: int, floor, raw_peaks: np.ndarray, params, hint=N
     return {"final_peaks": fin[:nf.value].copy(), "bpm_times": bt[:nb.value].copy(), "bpm": bv[:nb.value].copy(),
             "start_bpm": float(pas[0]), "peak_time": nan2none(pas[1]), "recovery_time": nan2none(pas[2]),
             "tags": tags[:len(pk)].copy()}
+
+
+def beats_batch(results, params, hint=None, threads: int = 1) -> list:
+    """bpmx_beats_batch over per-file dicts (env, floor, peaks, sr) on
+    ``threads`` native host threads; one call, no per-file Python work beyond
+    collecting pointers.  Entries with ``error`` pass through."""
+    L = load()
+    bp = params if isinstance(params, BeatParams) else beat_params(params)
+    idx = [k for k, r in enumerate(results) if "error" not in r]
+    out = list(results)
+    F = len(idx)
+    if F == 0:
+        return out
+    keep, envp, flp, pkp, ne, npk, srs = [], [], [], [], [], [], []
+    finb, btb, bvb, tagb = [], [], [], []
+    for k in idx:
+        r = results[k]
+        e = np.ascontiguousarray(r["env"], dtype=np.float64)
+        fl = np.ascontiguousarray(getattr(r["floor"], "values", r["floor"]), dtype=np.float64)
+        pk = np.ascontiguousarray(r["peaks"], dtype=np.int64)
+        m = max(len(pk), 1)
+        bufs = (np.empty(m, np.int64), np.empty(m), np.empty(m), np.empty(m, np.int8))
+        keep += [e, fl, pk]
+        envp.append(e.ctypes.data); flp.append(fl.ctypes.data); pkp.append(pk.ctypes.data)
+        ne.append(e.size); npk.append(len(pk)); srs.append(int(r["sr"]))
+        finb.append(bufs[0]); btb.append(bufs[1]); bvb.append(bufs[2]); tagb.append(bufs[3])
+    ptr = lambda lst: (ctypes.c_void_p * F)(*lst)  # noqa: E731
+    data = lambda bl: ptr([b.ctypes.data for b in bl])  # noqa: E731
+    ne_a, npk_a = np.array(ne, np.int64), np.array(npk, np.int64)
+    sr_a = np.array(srs, np.int32)
+    nf, nb, st = np.zeros(F, np.int64), np.zeros(F, np.int64), np.zeros(F, np.int32)
+    pas = np.empty((F, 3))
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = L.bpmx_beats_batch(F, ptr(envp), p(ne_a), ptr(flp), ptr(pkp), p(npk_a), p(sr_a), ctypes.byref(bp),
+                            float("nan") if hint is None else float(hint), int(threads), data(finb), p(nf),
+                            data(btb), data(bvb), p(nb), p(pas), data(tagb), p(st))
+    if rc != OK:
+        raise ValueError(f"bpmx_beats_batch failed ({rc})")
+    nan2none = lambda x: None if x != x else float(x)  # noqa: E731
+    for j, k in enumerate(idx):
+        if st[j] == E_FEW_PEAKS:
+            out[k] = {"error": KeyError("dynamic_noise_floor_series")}
+        elif st[j] != OK:
+            raise ValueError(f"bpmx_beats failed ({st[j]}) for recording {k}")
+        else:
+            out[k] = {"final_peaks": finb[j][:nf[j]], "bpm_times": btb[j][:nb[j]], "bpm": bvb[j][:nb[j]],
+                      "start_bpm": float(pas[j, 0]), "peak_time": nan2none(pas[j, 1]),
+                      "recovery_time": nan2none(pas[j, 2]), "tags": tagb[j][:npk[j]]}
+    return out

@@ -716,15 +716,4 @@ def analyze_fast(results: Sequence[Dict], params: Dict, start_bpm_hint: Optional
     as ``analyze_recording`` (tests/test_host_beats.py); HRV, slopes, reports
     and the plot stay with analyze_recording."""
     from . import _host
-    bp = _host.beat_params(params)
-
-    def one(r):
-        if "error" in r:
-            return r
-        return _host.beats(r["env"], r["sr"], r["floor"], r["peaks"], bp, start_bpm_hint)
-
-    if threads <= 1 or len(results) < 2:
-        return [one(r) for r in results]
-    from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(threads) as ex:
-        return list(ex.map(one, results))
+    return _host.beats_batch(list(results), params, start_bpm_hint, threads=threads)

@@ -27,6 +27,8 @@
 #include <cstdint>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "../../include/bpmx_host.h"
@@ -522,6 +524,29 @@ int bpmx_beats(const double *env, int64_t n_env, const double *floor, const int6
         for (size_t i = 0; i < curve.size(); ++i) { bpm_t_out[i] = t_ok[i]; bpm_out[i] = curve[i]; }
         *n_bpm = (int64_t)curve.size();
     }
+    return BPMX_HOST_OK;
+}
+
+int bpmx_beats_batch(int32_t n_files, const double *const *env, const int64_t *n_env, const double *const *floor,
+                     const int64_t *const *peaks, const int64_t *n_peaks, const int32_t *sr,
+                     const bpmx_beat_params *params, double start_bpm_hint, int32_t threads,
+                     int64_t *const *final_out, int64_t *n_final, double *const *bpm_t_out, double *const *bpm_out,
+                     int64_t *n_bpm, double *pass_out, int8_t *const *tags_out, int32_t *status) {
+    if (n_files < 0 || !env || !n_env || !floor || !peaks || !n_peaks || !sr || !params || !final_out || !n_final ||
+        !bpm_t_out || !bpm_out || !n_bpm || !status)
+        return BPMX_HOST_E_ARG;
+    std::atomic<int32_t> next{0};
+    auto work = [&]() {
+        for (int32_t f; (f = next.fetch_add(1)) < n_files;)
+            status[f] = bpmx_beats(env[f], n_env[f], floor[f], peaks[f], n_peaks[f], sr[f], params, start_bpm_hint,
+                                   final_out[f], &n_final[f], bpm_t_out[f], bpm_out[f], &n_bpm[f],
+                                   pass_out ? pass_out + 3 * (int64_t)f : nullptr, tags_out ? tags_out[f] : nullptr);
+    };
+    const int32_t nt = threads < 1 ? 1 : (threads > n_files ? (n_files > 0 ? n_files : 1) : threads);
+    std::vector<std::thread> pool;
+    for (int32_t t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto &th : pool) th.join();
     return BPMX_HOST_OK;
 }
 

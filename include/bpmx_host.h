@@ -64,6 +64,15 @@ int bpmx_beats(const double *env, int64_t n_env, const double *floor, const int6
                int64_t *n_final, double *bpm_t_out, double *bpm_out, int64_t *n_bpm, double *pass_out,
                int8_t *tags_out);
 
+/* bpmx_beats over many recordings on `threads` host threads (a work queue of
+ * files): per-file pointers and sizes, per-file status (bpmx_host_status);
+ * pass_out is [n_files][3]. */
+int bpmx_beats_batch(int32_t n_files, const double *const *env, const int64_t *n_env, const double *const *floor,
+                     const int64_t *const *peaks, const int64_t *n_peaks, const int32_t *sr,
+                     const bpmx_beat_params *params, double start_bpm_hint, int32_t threads,
+                     int64_t *const *final_out, int64_t *n_final, double *const *bpm_t_out, double *const *bpm_out,
+                     int64_t *n_bpm, double *pass_out, int8_t *const *tags_out, int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,7 +61,7 @@ def test_host_library_exports_every_declared_symbol():
     txt = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                             "bpmx_host.h")).read()
     names = set(re.findall(r"^\s*int\s+(bpmx_\w+)\s*\(", txt, re.M))
-    assert names == {"bpmx_host_abi_version", "bpmx_beats"}
+    assert names == {"bpmx_host_abi_version", "bpmx_beats", "bpmx_beats_batch"}
     L = H.load()
     for n in names:
         assert hasattr(L, n)
