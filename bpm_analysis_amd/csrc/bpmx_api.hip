@@ -343,6 +343,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     bs.env = O->env; bs.doff = d_doff; bs.boff = d_boff; bs.active = d_active; bs.n_files = F;
     bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
     const bool long_files = maxnd > QR_MAX;
+    const bool fp_global = (P->options & BPMX_OPT_PEAKS_GLOBAL) != 0;
     bool noise_lazy = false;
     if (long_files) {
         /* a few workgroups per long recording when the batch is small */
@@ -388,8 +389,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5;
             a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
-            LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
-            a.only = fp_fb;                   /* recordings with more maxima than the LDS kernel holds */
+            if (!fp_global) {
+                LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
+                a.only = fp_fb;               /* recordings with more maxima than the LDS kernel holds */
+            }
             LAUNCH(ctx, s, "k_find_peaks[troughs,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
         }
         if (bad_window)
@@ -553,8 +556,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0;
         a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
-        LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
-        a.only = fp_fb;
+        if (!fp_global) {
+            LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
+            a.only = fp_fb;
+        }
         LAUNCH(ctx, s, "k_find_peaks[peaks,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
     }
     return BPMX_OK;

@@ -86,8 +86,10 @@ enum bpmx_option {
                                        recordings of > 512 troughs (test/diagnostic; default ranks per window) */
     BPMX_OPT_ROLLQ_GLOBAL = 64,  /* force the global-memory sorted-union rolling quantile (test/diagnostic;
                                     default: only for windows beyond the LDS kernel on long recordings) */
-    BPMX_OPT_NATIVE_DMA = 128    /* native mode, int16 mono without the matrix-core path: the LDS-DMA f64
+    BPMX_OPT_NATIVE_DMA = 128,   /* native mode, int16 mono without the matrix-core path: the LDS-DMA f64
                                     block kernel (default for int16 stereo) instead of the register-prefetch one */
+    BPMX_OPT_PEAKS_GLOBAL = 256  /* find_peaks by sample walks over global memory (k_find_peaks) for every
+                                    recording instead of the LDS-resident extrema (test/diagnostic) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

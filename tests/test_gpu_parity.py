@@ -335,6 +335,29 @@ def test_rollq_pruning_exact(det):
         assert _same(a["troughs"], ot)
 
 
+def test_find_peaks_kernels_agree(det):
+    """find_peaks with prominences from the LDS-resident local extrema
+    (k_find_peaks_lds, default) equals the sample walks over global memory
+    (k_find_peaks, BPMX_OPT_PEAKS_GLOBAL) bit for bit, troughs and peaks, on
+    every floor-stress envelope plus plateau-heavy and > 3072-maxima ones
+    (those the LDS kernel hands over), all in one ragged batch."""
+    from bpm_analysis_amd import _native as N
+    params = dict(G.BASE_PARAMS)
+    rng = np.random.default_rng(11)
+    envs = [e for e, sr in _floor_envelopes() if sr == 302]
+    n = 18124
+    envs.append(np.round(rng.random(n) * 4) + 100 * (np.arange(n) % 300 == 0))     # plateaus, ties
+    envs.append(rng.random(n) * 10)                                                 # ~6000 maxima
+    envs.append(np.repeat(rng.random(n // 8), 8))                                   # flat runs
+    stages = N.STAGE_FLOOR | N.STAGE_PEAKS
+    a = det.run_env_host(envs, 302, params, stages)
+    b = det.run_env_host(envs, 302, params, stages, options=N.OPT_PEAKS_GLOBAL)
+    for x, y in zip(a, b):
+        assert _same(x["troughs"], y["troughs"])
+        assert _same(x["peaks"], y["peaks"])
+        assert _same(x["floor"], y["floor"])
+
+
 @pytest.mark.parametrize("fs", [44100, 22050, 48000])
 def test_native_block_kernels_agree(det, fs):
     """The exact-integer matrix-core block projections (default for int16 mono,
