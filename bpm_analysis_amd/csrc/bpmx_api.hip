@@ -344,6 +344,47 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
     const bool long_files = maxnd > QR_MAX;
     const bool fp_global = (P->options & BPMX_OPT_PEAKS_GLOBAL) != 0;
+    /* find_peaks: k_find_peaks_lds for every recording it holds; the others
+     * (longer than FPL_NMIN, or more than FL_MC maxima) take the multi-
+     * workgroup k_fpl_* path when the batch has long recordings, else the
+     * one-workgroup k_find_peaks (BPMX_OPT_PEAKS_GLOBAL: k_find_peaks for all) */
+    const bool fp_long = !fp_global && maxnd > FPL_NMIN;
+    FplArgs fl{};
+    if (fp_long) {
+        fl.nu = (int32_t)((maxnd - 2 + FPL_U - 1) / FPL_U);
+        fl.cnt = (int32_t *)ctx->buf("fpl_cnt", (size_t)F * fl.nu * 8, &rc);
+        fl.mtot = (int32_t *)ctx->buf("fpl_mtot", (size_t)F * 4, &rc);
+        fl.mp = (int32_t *)ctx->buf("fpl_mp", (size_t)sumnd * 4, &rc);
+        fl.mh = (double *)ctx->buf("fpl_mh", (size_t)sumnd * 8, &rc);
+        fl.vv = (double *)ctx->buf("fpl_vv", (size_t)(sumnd + F) * 8, &rc);
+        const size_t n32 = (size_t)(sumnd >> 5) + 4 * (size_t)F + 4, n1k = (size_t)(sumnd >> 10) + 4 * (size_t)F + 4;
+        double *b32 = (double *)ctx->buf("fpl_b32", n32 * 3 * 8, &rc);
+        double *b1k = (double *)ctx->buf("fpl_b1k", n1k * 3 * 8, &rc);
+        if (rc != BPMX_OK) return rc;
+        fl.b32h = b32; fl.b32l = b32 + n32; fl.b32r = b32 + 2 * n32;
+        fl.b1kh = b1k; fl.b1kl = b1k + n1k; fl.b1kr = b1k + 2 * n1k;
+    }
+    const dim3 g_unit((unsigned)((((maxnd - 2 + FPL_U - 1) / FPL_U) + 3) / 4), (unsigned)F);
+    const dim3 g_prom((unsigned)((maxnd / 2 + 1 + 255) / 256), (unsigned)F);
+#define FIND_PEAKS(A, TAG)                                                                                  \
+    do {                                                                                                   \
+        (A).vcand = vcand; (A).fallback = fp_fb; (A).only = nullptr;                                      \
+        (A).lds_nmax = fp_long ? FPL_NMIN : INT64_MAX;                                                     \
+        if (!fp_global) {                                                                                  \
+            LAUNCH(ctx, s, "k_find_peaks[" TAG "]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, (A));    \
+            (A).only = fp_fb;             /* recordings the LDS kernel hands over */                       \
+        }                                                                                                  \
+        if (fp_long) {                                                                                     \
+            LAUNCH(ctx, s, "k_fpl_scan[" TAG "]", k_fpl_scan, g_unit, dim3(256), 0, s, (A), fl);          \
+            LAUNCH(ctx, s, "k_fpl_place[" TAG "]", k_fpl_place, dim3(F), dim3(256), 0, s, (A), fl);       \
+            LAUNCH(ctx, s, "k_fpl_fill[" TAG "]", k_fpl_fill, g_unit, dim3(256), 0, s, (A), fl);          \
+            LAUNCH(ctx, s, "k_fpl_distance[" TAG "]", k_fpl_distance, dim3(F), dim3(1024), 0, s, (A), fl);\
+            LAUNCH(ctx, s, "k_fpl_prom[" TAG "]", k_fpl_prom, g_prom, dim3(256), 0, s, (A), fl);          \
+            LAUNCH(ctx, s, "k_fpl_compact[" TAG "]", k_fpl_compact, dim3(F), dim3(1024), 0, s, (A), fl);  \
+        } else {                                                                                           \
+            LAUNCH(ctx, s, "k_find_peaks[" TAG ",gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, (A));     \
+        }                                                                                                  \
+    } while (0)
     bool noise_lazy = false;
     if (long_files) {
         /* a few workgroups per long recording when the batch is small */
@@ -388,12 +429,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5;
-            a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
-            if (!fp_global) {
-                LAUNCH(ctx, s, "k_find_peaks[troughs]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
-                a.only = fp_fb;               /* recordings with more maxima than the LDS kernel holds */
-            }
-            LAUNCH(ctx, s, "k_find_peaks[troughs,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+            FIND_PEAKS(a, "troughs");
         }
         if (bad_window)
             LAUNCH(ctx, s, "k_flag_window", k_flag_window, dim3((F + 255) / 256), dim3(256), 0, s, F, d_run1,
@@ -555,13 +591,9 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0;
-        a.vcand = vcand; a.fallback = fp_fb; a.only = nullptr;
-        if (!fp_global) {
-            LAUNCH(ctx, s, "k_find_peaks[peaks]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, a);
-            a.only = fp_fb;
-        }
-        LAUNCH(ctx, s, "k_find_peaks[peaks,gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, a);
+        FIND_PEAKS(a, "peaks");
     }
+#undef FIND_PEAKS
     return BPMX_OK;
 }
 

@@ -71,11 +71,48 @@ struct PeakArgs {
     int32_t run_min;
     int32_t *vcand;        /* k_find_peaks_lds: scratch [sumNd], valley positions */
     int32_t *fallback;     /* k_find_peaks_lds: [F] out, 1 = too many maxima for LDS (k_find_peaks takes it) */
-    const int32_t *only;   /* k_find_peaks: [F] or null, process only recordings with only[f] != 0 */
+    const int32_t *only;   /* k_find_peaks / k_fpl_*: [F] or null, process only recordings with only[f] != 0 */
+    int64_t lds_nmax;      /* k_find_peaks_lds: hand recordings longer than this over (fallback = 1) */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
 };
+
+/* find_peaks candidate states (k_find_peaks, k_find_peaks_lds, k_fpl_*) */
+enum { ST_UNDECIDED = 0, ST_KEPT = 1, ST_REMOVED = 2, ST_FINAL = 3 };
+
+__device__ __forceinline__ uint8_t ld_state(const uint8_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_state(uint8_t *p, uint8_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr int FL_MC = 3072;          /* k_find_peaks_lds: local maxima held in LDS */
+
+/* find_peaks for long recordings (k_peaks_long.hip): the local-extrema
+ * formulation of k_find_peaks_lds with the extrema in global scratch and the
+ * per-sample and per-maximum phases spread over many workgroups */
+constexpr int FPL_U = 1024;          /* positions per scan unit (one wave) */
+constexpr int64_t FPL_NMIN = 65536;  /* recordings longer than this take the k_fpl_* path */
+struct FplArgs {
+    int32_t nu;            /* scan units per recording (max over the batch) */
+    int32_t *cnt;          /* [F][nu][2] maxima / valley counts per unit, then (k_fpl_place) maxima offsets */
+    int32_t *mtot;         /* [F] local maxima per recording */
+    int32_t *mp;           /* [sumNd] maxima positions (dense per recording at doff) */
+    double *mh;            /* [sumNd] maxima values (sign applied) */
+    double *vv;            /* [sumNd + F] gap valleys: vv[g] = valley between maxima g-1 and g */
+    double *b32h, *b32l, *b32r;    /* per 32 maxima: max height, min vv[k+1], min vv[k] */
+    double *b1kh, *b1kl, *b1kr;    /* per 1024 maxima: the same */
+};
+__host__ __device__ inline int64_t fpl_b32_off(int64_t d0, int f) { return (d0 >> 5) + 4 * (int64_t)f; }
+__host__ __device__ inline int64_t fpl_b1k_off(int64_t d0, int f) { return (d0 >> 10) + 4 * (int64_t)f; }
+__global__ void k_fpl_scan(PeakArgs A, FplArgs L);
+__global__ void k_fpl_place(PeakArgs A, FplArgs L);
+__global__ void k_fpl_fill(PeakArgs A, FplArgs L);
+__global__ void k_fpl_distance(PeakArgs A, FplArgs L);
+__global__ void k_fpl_prom(PeakArgs A, FplArgs L);
+__global__ void k_fpl_compact(PeakArgs A, FplArgs L);
 
 struct InterpArgs {
     const double *env;

@@ -356,15 +356,6 @@ __device__ void prominence_waves(const double *e, double sg, int64_t n, const do
     for (int c = 0; c < NP; ++c) prom[c] = xpp[c] - fmax(lm[c], rm[c]);
 }
 
-enum { ST_UNDECIDED = 0, ST_KEPT = 1, ST_REMOVED = 2, ST_FINAL = 3 };
-
-__device__ __forceinline__ uint8_t ld_state(const uint8_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void st_state(uint8_t *p, uint8_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 constexpr int FP_T = 1024;
 #ifndef BPMX_FP_NP
 #define BPMX_FP_NP 2      /* prominences per wave per round (their loads overlap) */
@@ -623,7 +614,6 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
  * maxima (native mode) to ~2400 (reference mode); a recording with more than
  * FL_MC maxima is flagged for k_find_peaks.  Everything else — height,
  * distance rounds, prominence threshold, ordered output — is k_find_peaks'. */
-constexpr int FL_MC = 3072;
 
 __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     const int f = blockIdx.x;
@@ -635,6 +625,10 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     }
     const int64_t d0 = A.doff[f];
     const int64_t n = A.doff[f + 1] - d0;
+    if (n > A.lds_nmax) {                                    /* long recording: the k_fpl_* kernels */
+        if (tid == 0) A.fallback[f] = 1;
+        return;
+    }
     const double *e = A.env + d0;
     const double *h = A.height ? A.height + d0 : nullptr;
     const double sg = A.sign;

@@ -1,0 +1,292 @@
+/*
+ * k_peaks_long.hip — find_peaks (bpm_analysis.py:1066-1070 troughs, :223-229
+ * raw peaks: scipy.signal.find_peaks with height, distance, prominence) for
+ * long recordings, spread over many workgroups per recording.
+ *
+ * Same formulation as k_find_peaks_lds (k_detect.hip): the local maxima
+ * (scipy _local_maxima_1d, plateau midpoints) and the one valley between each
+ * pair of consecutive maxima determine every prominence:
+ *     left_min(j)  = min(vv[k* + 1 .. j])   k* = nearest maximum left of j higher than j (or -1)
+ *     right_min(j) = min(vv[j + 1 .. k'])   k' = nearest maximum right of j higher than j (or M)
+ * with vv[g] the valley of gap g (between maxima g-1 and g; vv[0] and vv[M]
+ * include x[0] and x[n-1]).  Here the extrema live in global scratch:
+ *   k_fpl_scan      one wave per 1024 positions: maxima and valley starts,
+ *                   compacted per unit (coalesced env reads)
+ *   k_fpl_place     per recording: unit offsets of the maxima, M, edge gaps
+ *   k_fpl_fill      one wave per unit: dense maxima (position, value, state
+ *                   after the height filter) and gap valleys
+ *   k_fpl_distance  per recording: 32- and 1024-maxima block summaries, then
+ *                   the distance rounds (k_find_peaks' rule: a candidate is
+ *                   decided once every higher-priority neighbour within the
+ *                   distance is)
+ *   k_fpl_prom      one thread per kept maximum: walk the maxima outwards to
+ *                   the nearest higher one, whole blocks of no-higher maxima
+ *                   skipped through their summaries
+ *   k_fpl_compact   per recording: ordered output, counts
+ * Selected recordings: A.only[f] != 0 (k_find_peaks_lds hands over those
+ * longer than A.lds_nmax or with more than FL_MC maxima).
+ */
+#include "bpmx_common.h"
+#include "bpmx_kernels.h"
+
+namespace bpmx {
+
+namespace {
+__device__ __forceinline__ bool fpl_selected(const PeakArgs &A, int f) {
+    return f < A.n_files && A.active[f] && (!A.only || A.only[f]);
+}
+__device__ __forceinline__ int fpl_units(int64_t n) {
+    return n > 2 ? (int)((n - 2 + FPL_U - 1) / FPL_U) : 0;
+}
+}  // namespace
+
+constexpr int FPL_T = 256;   /* threads of the per-unit kernels: 4 units per workgroup */
+
+__global__ __launch_bounds__(FPL_T) void k_fpl_scan(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.y;
+    if (!fpl_selected(A, f)) return;
+    const int u = blockIdx.x * (FPL_T / 64) + wave_id(), lane = lane_id();
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    if (u >= fpl_units(n)) return;
+    const double *e = A.env + d0;
+    const double sg = A.sign;
+    const int64_t w0 = 1 + (int64_t)u * FPL_U, w1 = min<int64_t>(n - 1, w0 + FPL_U);
+    int32_t *mp_g = A.cand + d0 + (int64_t)u * FPL_U, *vp_g = A.vcand + d0 + (int64_t)u * FPL_U;
+    int cm = 0, cv = 0;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int64_t b = w0; b < w1; b += 64) {
+        const int64_t i = b + lane;
+        bool ism = false, isv = false;
+        int32_t pk = 0;
+        if (i < w1) {
+            const double xi = sg * e[i], xl = sg * e[i - 1];
+            if (xl != xi) {
+                int64_t ia = i + 1;
+                while (ia < n - 1 && sg * e[ia] == xi) ia++;
+                const double xr = sg * e[ia];
+                if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
+                else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)i; }
+            }
+        }
+        const unsigned long long bm = __ballot(ism), bv = __ballot(isv);
+        if (ism) mp_g[cm + __popcll(bm & lt)] = pk;
+        if (isv) vp_g[cv + __popcll(bv & lt)] = pk;
+        cm += __popcll(bm);
+        cv += __popcll(bv);
+    }
+    if (lane == 0) {
+        int32_t *c = L.cnt + ((int64_t)f * L.nu + u) * 2;
+        c[0] = cm;
+        c[1] = cv;
+    }
+}
+
+/* per recording: exclusive scan of the units' maxima counts (in place), M,
+ * and the edge gaps' sample terms */
+__global__ __launch_bounds__(FPL_T) void k_fpl_place(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.x;
+    if (!fpl_selected(A, f)) return;
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    const int nu = fpl_units(n), tid = threadIdx.x;
+    __shared__ int sh[FPL_T / 64 + 1];
+    int32_t *c = L.cnt + (int64_t)f * L.nu * 2;
+    int run = 0;
+    for (int u0 = 0; u0 < nu; u0 += FPL_T) {
+        const int u = u0 + tid;
+        const int v = u < nu ? c[2 * u] : 0;
+        int tot;
+        const int off = block_scan_int<FPL_T>(v, sh, &tot);
+        if (u < nu) c[2 * u] = run + off;
+        run += tot;
+    }
+    if (tid == 0) {
+        L.mtot[f] = run;
+        double *vv = L.vv + d0 + f;
+        if (n > 0) {
+            vv[0] = A.sign * A.env[d0];
+            if (run > 0) vv[run] = A.sign * A.env[d0 + n - 1];
+        }
+    }
+}
+
+__global__ __launch_bounds__(FPL_T) void k_fpl_fill(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.y;
+    if (!fpl_selected(A, f)) return;
+    const int u = blockIdx.x * (FPL_T / 64) + wave_id(), lane = lane_id();
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    const int nu = fpl_units(n);
+    if (u >= nu) return;
+    const double *e = A.env + d0;
+    const double *h = A.height ? A.height + d0 : nullptr;
+    const double sg = A.sign;
+    const int32_t *c = L.cnt + (int64_t)f * L.nu * 2;
+    const int M = L.mtot[f];
+    const int off = c[2 * u], cm = (u + 1 < nu ? c[2 * u + 2] : M) - off, cv = c[2 * u + 1];
+    const int32_t *mp_u = A.cand + d0 + (int64_t)u * FPL_U, *vp_u = A.vcand + d0 + (int64_t)u * FPL_U;
+    int32_t *mp = L.mp + d0;
+    double *mh = L.mh + d0, *vv = L.vv + d0 + f;
+    uint8_t *st = A.state + d0;
+    const uint8_t open = A.distance > 1 ? ST_UNDECIDED : ST_KEPT;
+    for (int t = lane; t < cm; t += 64) {
+        const int32_t p = mp_u[t];
+        const double xv = sg * e[p];
+        mp[off + t] = p;
+        mh[off + t] = xv;
+        st[off + t] = (!h || h[p] <= xv) ? open : ST_REMOVED;   /* height filter */
+    }
+    for (int t = lane; t < cv; t += 64) {
+        const int32_t pv = vp_u[t];
+        int lo = 0, hi = cm;                                 /* the unit's maxima before the valley */
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (mp_u[mid] < pv) lo = mid + 1; else hi = mid; }
+        const int g = off + lo;
+        const double val = sg * e[pv];
+        if (g == 0 || g == M) vv[g] = fmin(vv[g], val);      /* edge gaps: at most one valley each */
+        else vv[g] = val;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_fpl_distance(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.x;
+    if (!fpl_selected(A, f)) return;
+    const int tid = threadIdx.x;
+    const int64_t d0 = A.doff[f];
+    const int M = L.mtot[f];
+    const int32_t *mp = L.mp + d0;
+    const double *mh = L.mh + d0, *vv = L.vv + d0 + f;
+    uint8_t *st = A.state + d0;
+    const double INF = __builtin_inf();
+    __shared__ int s_flag;
+    /* block summaries for the prominence walks */
+    double *b32h = L.b32h + fpl_b32_off(d0, f), *b32l = L.b32l + fpl_b32_off(d0, f), *b32r = L.b32r + fpl_b32_off(d0, f);
+    const int NB32 = (M + 31) >> 5, NB1K = (M + 1023) >> 10;
+    for (int b = tid; b < NB32; b += 1024) {
+        double hx = -INF, vl = INF, vr = INF;
+        const int k1 = min(M, b * 32 + 32);
+        for (int k = b * 32; k < k1; ++k) {
+            hx = fmax(hx, mh[k]);
+            vl = fmin(vl, vv[k + 1]);
+            vr = fmin(vr, vv[k]);
+        }
+        b32h[b] = hx;
+        b32l[b] = vl;
+        b32r[b] = vr;
+    }
+    __syncthreads();
+    {
+        double *bh = L.b1kh + fpl_b1k_off(d0, f), *bl = L.b1kl + fpl_b1k_off(d0, f), *br = L.b1kr + fpl_b1k_off(d0, f);
+        for (int B = tid; B < NB1K; B += 1024) {
+            double hx = -INF, vl = INF, vr = INF;
+            const int b1 = min(NB32, B * 32 + 32);
+            for (int b = B * 32; b < b1; ++b) {
+                hx = fmax(hx, b32h[b]);
+                vl = fmin(vl, b32l[b]);
+                vr = fmin(vr, b32r[b]);
+            }
+            bh[B] = hx;
+            bl[B] = vl;
+            br[B] = vr;
+        }
+    }
+    const int64_t dist = A.distance;
+    if (dist <= 1) return;
+    /* every round decides at least the highest-priority undecided candidate */
+    for (int round = 0; round <= M; ++round) {
+        if (tid == 0) s_flag = 0;
+        __syncthreads();
+        bool pending = false;
+        for (int j = tid; j < M; j += 1024) {
+            if (ld_state(&st[j]) != ST_UNDECIDED) continue;
+            const int64_t pj = mp[j];
+            const double vj = mh[j];
+            bool killed = false, blocked = false;
+            for (int k = j - 1; k >= 0 && pj - mp[k] < dist; --k) {
+                if (mh[k] > vj) {                            /* earlier index wins only when strictly higher */
+                    const uint8_t s = ld_state(&st[k]);
+                    if (s == ST_KEPT) { killed = true; break; }
+                    if (s == ST_UNDECIDED) blocked = true;
+                }
+            }
+            if (!killed) {
+                for (int k = j + 1; k < M && mp[k] - pj < dist; ++k) {
+                    if (mh[k] >= vj) {                       /* later index wins ties (stable argsort order) */
+                        const uint8_t s = ld_state(&st[k]);
+                        if (s == ST_KEPT) { killed = true; break; }
+                        if (s == ST_UNDECIDED) blocked = true;
+                    }
+                }
+            }
+            if (killed) st_state(&st[j], ST_REMOVED);
+            else if (!blocked) st_state(&st[j], ST_KEPT);
+            else pending = true;
+        }
+        if (pending) s_flag = 1;
+        __syncthreads();
+        const int again = s_flag;
+        __syncthreads();
+        if (!again) break;
+    }
+}
+
+__global__ __launch_bounds__(FPL_T) void k_fpl_prom(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.y;
+    if (!fpl_selected(A, f)) return;
+    const int j = blockIdx.x * FPL_T + threadIdx.x;
+    const int M = L.mtot[f];
+    if (j >= M) return;
+    const int64_t d0 = A.doff[f];
+    uint8_t *st = A.state + d0;
+    if (st[j] != ST_KEPT) return;
+    const double *mh = L.mh + d0, *vv = L.vv + d0 + f;
+    const int64_t o32 = fpl_b32_off(d0, f), o1k = fpl_b1k_off(d0, f);
+    const double *b32h = L.b32h + o32, *b32l = L.b32l + o32, *b32r = L.b32r + o32;
+    const double *bkh = L.b1kh + o1k, *bkl = L.b1kl + o1k, *bkr = L.b1kr + o1k;
+    const double INF = __builtin_inf();
+    const double hj = mh[j];
+    double lmin = INF, rmin = INF;
+    for (int k = j - 1;;) {
+        if (k < 0) { lmin = fmin(lmin, vv[0]); break; }
+        if ((k & 1023) == 1023 && bkh[k >> 10] <= hj) { lmin = fmin(lmin, bkl[k >> 10]); k -= 1024; continue; }
+        if ((k & 31) == 31 && b32h[k >> 5] <= hj) { lmin = fmin(lmin, b32l[k >> 5]); k -= 32; continue; }
+        lmin = fmin(lmin, vv[k + 1]);
+        if (mh[k] > hj) break;
+        --k;
+    }
+    for (int k = j + 1;;) {
+        if (k >= M) { rmin = fmin(rmin, vv[M]); break; }
+        if ((k & 1023) == 0 && k + 1023 < M && bkh[k >> 10] <= hj) { rmin = fmin(rmin, bkr[k >> 10]); k += 1024; continue; }
+        if ((k & 31) == 0 && k + 31 < M && b32h[k >> 5] <= hj) { rmin = fmin(rmin, b32r[k >> 5]); k += 32; continue; }
+        rmin = fmin(rmin, vv[k]);
+        if (mh[k] > hj) break;
+        ++k;
+    }
+    const double prom = hj - fmax(lmin, rmin);
+    const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
+    st[j] = thr <= prom ? ST_FINAL : ST_REMOVED;
+}
+
+__global__ __launch_bounds__(1024) void k_fpl_compact(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.x;
+    if (!fpl_selected(A, f)) return;
+    const int tid = threadIdx.x;
+    const int64_t d0 = A.doff[f];
+    const int M = L.mtot[f];
+    const int32_t *mp = L.mp + d0;
+    const uint8_t *st = A.state + d0;
+    __shared__ int sh[1024 / 64 + 1];
+    int64_t *out = A.out + d0;
+    int w = 0;
+    for (int q0 = 0; q0 < M; q0 += 1024) {
+        const int j = q0 + tid;
+        const bool keep = j < M && st[j] == ST_FINAL;
+        int tot;
+        const int off = block_scan_flag<1024>(keep, sh, &tot);
+        if (keep) out[w + off] = mp[j];
+        w += tot;
+    }
+    if (tid == 0) {
+        A.nout[f] = w;
+        if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
+    }
+}
+
+}  // namespace bpmx

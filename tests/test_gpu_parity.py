@@ -356,6 +356,28 @@ def test_find_peaks_kernels_agree(det):
         assert _same(x["troughs"], y["troughs"])
         assert _same(x["peaks"], y["peaks"])
         assert _same(x["floor"], y["floor"])
+    # with recordings beyond 65536 samples in the batch, the long ones and the
+    # short ones with > 3072 maxima take the multi-workgroup k_fpl_* path
+    m = 200_000
+    t = np.arange(m)
+    beat = np.maximum(0.0, np.sin(2 * np.pi * t / 250.0)) ** 8
+    long_envs = [
+        10.0 + 0.001 * t + 3000 * beat + rng.random(m),                     # rising: long prominence walks
+        np.concatenate([np.full(70_000, 5.0), 300 * beat[:70_000] + 20]),    # flat head: edge gaps
+        np.round(rng.random(m) * 3) + 200 * (t % 700 == 0),                 # plateaus and ties everywhere
+        300 * beat[:66_000] + rng.random(66_000),
+    ]
+    envs2 = long_envs + envs[-3:]
+    a = det.run_env_host(envs2, 302, params, stages)
+    b = det.run_env_host(envs2, 302, params, stages, options=N.OPT_PEAKS_GLOBAL)
+    for x, y in zip(a, b):
+        assert _same(x["troughs"], y["troughs"])
+        assert _same(x["peaks"], y["peaks"])
+        assert _same(x["floor"], y["floor"])
+    d = O.derive(302, params)
+    of, ot, _ = O.noise_floor(long_envs[0], d, params)
+    assert _same(a[0]["troughs"], ot)
+    assert _same(a[0]["peaks"], O.raw_peaks(long_envs[0], of, d, params))
 
 
 @pytest.mark.parametrize("fs", [44100, 22050, 48000])
