@@ -30,6 +30,8 @@ struct bpmx_ctx {
     /* native-mode block-state tables (host copies back the async uploads) */
     std::vector<int64_t> nat_key;
     std::vector<double> nat_tab;
+    std::vector<int64_t> blu_key;     /* Bluestein group geometry of the FFT(b) tables in "blu_b" */
+    std::vector<int32_t> blu_files;   /* host copy of the Bluestein groups' file lists */
     std::vector<int32_t> nat_fused;   /* per-file: envelope done by the fused Hilbert kernel (host copy outlives async uploads) */
     std::vector<int64_t> nat_boff;              /* block offsets | per-file tile offsets */
     std::vector<int64_t> nat_tkey;              /* tile-list geometry key */

@@ -1589,6 +1589,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     fused.assign(F, 0);
     bool side_used[bpmx_ctx::NSIDE] = {};
     bool forked = false;
+    std::vector<int32_t> blu;
     int f0 = 0;
     while (f0 < F) {
         const int64_t nd = doff[f0 + 1] - doff[f0];
@@ -1616,7 +1617,10 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             }
         }
         if (rc != BPMX_OK) return rc;
-        if (nd > 15) {
+        if (nd > 15 && !(P->options & BPMX_OPT_HILBERT_R2C)) {   /* batched Bluestein, after the loop */
+            need_env = true;
+            for (int f = f0; f < f1; ++f) blu.push_back(f);
+        } else if (nd > 15) {
             need_env = true;
             FftPlans *pl = nullptr;
             if ((rc = get_plans(ctx->device, nd, f1 - f0, &pl)) != BPMX_OK) return rc;
@@ -1660,6 +1664,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         }
         f0 = f1;
     }
+    if ((rc = bluestein_hilbert(ctx, s, yd, hb, doff, d_doff, blu)) != BPMX_OK) return rc;
     for (int i = 0; i < bpmx_ctx::NSIDE; ++i)       /* join the side streams back into s */
         if (side_used[i]) {
             HIP_TRY(hipEventRecord(ctx->side_join[i], ctx->side[i]));

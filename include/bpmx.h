@@ -88,8 +88,11 @@ enum bpmx_option {
                                     default: only for windows beyond the LDS kernel on long recordings) */
     BPMX_OPT_NATIVE_DMA = 128,   /* native mode, int16 mono without the matrix-core path: the LDS-DMA f64
                                     block kernel (default for int16 stereo) instead of the register-prefetch one */
-    BPMX_OPT_PEAKS_GLOBAL = 256  /* find_peaks by sample walks over global memory (k_find_peaks) for every
+    BPMX_OPT_PEAKS_GLOBAL = 256, /* find_peaks by sample walks over global memory (k_find_peaks) for every
                                     recording instead of the LDS-resident extrema (test/diagnostic) */
+    BPMX_OPT_HILBERT_R2C = 512   /* native mode, recordings outside the fused Hilbert kernel: one rocFFT
+                                    R2C/C2R plan per distinct length instead of the batched Bluestein
+                                    transform (test/diagnostic) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

@@ -410,9 +410,11 @@ def test_native_block_kernels_agree(det, fs):
 
 def test_fused_hilbert_matches_rocfft_and_oracle(det):
     """k_hilbert_env (in-LDS mixed-radix transform + rolling mean) against the
-    rocFFT path (BPMX_OPT_HILBERT_ROCFFT) and the oracle, on a ragged batch whose
-    Nd exercise radix 2 / 3 / 5 / 23 / 197 / 401 plans, a tiny plan, and odd or
-    large-prime Nd that fall back to rocFFT inside the same batch."""
+    batched Bluestein transform (BPMX_OPT_HILBERT_ROCFFT: every recording),
+    the per-length rocFFT R2C/C2R path (+ BPMX_OPT_HILBERT_R2C) and the oracle,
+    on a ragged batch whose Nd exercise radix 2 / 3 / 5 / 23 / 197 / 401 plans,
+    a tiny plan, and odd or large-prime Nd that fall back inside the same
+    batch (packed and unpacked Bluestein groups)."""
     import torch
     from bpm_analysis_amd import _native as N
     fs, ds = 44100, 146
@@ -423,16 +425,20 @@ def test_fused_hilbert_matches_rocfft_and_oracle(det):
     fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     params = dict(G.BASE_PARAMS)
     outs = []
-    for opt in (0, N.OPT_HILBERT_ROCFFT):
+    # default (fused where it plans, batched Bluestein elsewhere), Bluestein for
+    # all (BPMX_OPT_HILBERT_ROCFFT), per-length rocFFT R2C/C2R for all
+    for opt in (0, N.OPT_HILBERT_ROCFFT, N.OPT_HILBERT_ROCFFT | N.OPT_HILBERT_R2C):
         res = det.run(dev, fo, fs, params, mode="native", want_y=True, options=opt)
         torch.cuda.synchronize()
         outs.append(res.to_host())
-    for a, b, pcm in zip(outs[0], outs[1], recs):
-        scale = np.max(np.abs(b["env"]))
-        assert np.max(np.abs(a["env"] - b["env"])) <= 1e-12 * scale
+    for a, b, c, pcm in zip(outs[0], outs[1], outs[2], recs):
+        scale = np.max(np.abs(c["env"]))
+        assert np.max(np.abs(a["env"] - c["env"])) <= 1e-12 * scale
+        assert np.max(np.abs(b["env"] - c["env"])) <= 1e-12 * scale
         if len(pcm) > 5000 * ds:
             o = O.detect(pcm, fs, params, mode="native")
             _check_file(a, o, exact_env=False)
+            _check_file(b, o, exact_env=False)
 
 
 @pytest.mark.parametrize("name", ["ref_44k_60s_mono", "ref_44k_40s_clicks", "vulpine", "env_random_rough",

@@ -1,4 +1,4 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "find_peaks or c5 or c2 or long_noise or large_decimation or sharded" > gpurun_out/pt.log 2>&1; rc=$?; tail -25 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "hilbert or c5 or c2 or long_noise or large_decimation or sharded or dma" > gpurun_out/pt.log 2>&1; rc=$?; tail -25 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py --workload c5 --steps 5 --warmup 2 > gpurun_out/c5.log 2>&1; rc=$?; tail -3 gpurun_out/c5.log; exit $rc
