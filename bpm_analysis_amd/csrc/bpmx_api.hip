@@ -558,7 +558,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
             a.dec = tdec; a.exact = d_exact;
             a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
-            LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, DB_TRMAX / DB_T), dim3(DB_T), 0, s, a);
+            /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
+            const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
+            const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);
+            LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
         }
         if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {

@@ -675,29 +675,84 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int m = A.nraw[f];
     const int tid = threadIdx.x;
-    if (m > DB_TRMAX) {
-        if (tid == 0) A.exact[f] = 1;
-        return;
-    }
     /* Long recordings (> local_m troughs) rank each window's segments in
-     * place, so their troughs split over blockIdx.y chunks of DB_T; shorter
-     * ones build the recording-wide order once, in chunk 0. */
+     * place, so their troughs split over blockIdx.y chunks of DB_T, each
+     * staging only the troughs its windows reach; shorter ones build the
+     * recording-wide order once, in chunk 0. */
     const bool local = m > A.local_m;
     if (!local && blockIdx.y > 0) return;
     const int jc0 = local ? (int)blockIdx.y * DB_T : 0;
     const int jc1 = local ? (jc0 + DB_T < m ? jc0 + DB_T : m) : m;
     if (jc0 >= jc1) return;
+    if (!local && m > DB_TRMAX) {
+        if (tid == 0) A.exact[f] = 1;
+        return;
+    }
     const int64_t *raw = A.raw + d0;
     const double *env = A.env + d0;
+    const int64_t W = A.window, t0 = raw[0], off = (W - 1) / 2;
     if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; }
-    for (int j = tid; j < m; j += DB_T) {
-        s_tp[j] = (int32_t)raw[j];
-        s_tv[j] = env[raw[j]];
+    __syncthreads();
+    /* valid outputs (nobs >= min_periods) form one interval: with s >= t0 and
+     * e <= n (outputs [t0 + W - 1 - off, n - 1 - off]) nobs = W >= min_periods,
+     * so only the two edge stretches need the test */
+    {
+        const int64_t ma = t0 + W - 1 - off, mb = n - 1 - off;
+        int vf = INT_MAX, vl = -1;
+        auto test = [&](int64_t i) {
+            int64_t s, e;
+            win_bounds(i, n, W, s, e);
+            const int64_t lo = s > t0 ? s : t0;
+            if (e - lo >= A.min_periods && e > lo) { vf = min(vf, (int)i); vl = max(vl, (int)i); }
+        };
+        const int64_t ea = ma < n ? (ma > 0 ? ma : 0) : n;   /* [0, ea) */
+        const int64_t sb = mb + 1 > ea ? mb + 1 : ea;        /* [sb, n) */
+        for (int64_t i = tid; i < ea; i += DB_T) test(i);
+        for (int64_t i = sb + tid; i < n; i += DB_T) test(i);
+        if (tid == 0 && ea <= mb) { vf = min(vf, (int)ea); vl = max(vl, (int)min<int64_t>(mb, n - 1)); }
+        for (int o = 32; o > 0; o >>= 1) { vf = min(vf, __shfl_xor(vf, o)); vl = max(vl, __shfl_xor(vl, o)); }
+        if (lane_id() == 0) { atomicMin(&s_vf, vf); atomicMax(&s_vl, vl); }
     }
     __syncthreads();
-    const int64_t W = A.window, t0 = s_tp[0];
-    auto seg_lo = [&](int j) -> double { return j + 1 < m ? fmin(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
-    auto seg_hi = [&](int j) -> double { return j + 1 < m ? fmax(s_tv[j], s_tv[j + 1]) : s_tv[j]; };
+    const int vf = s_vf, vl = s_vl;
+    if (vl < vf) {                                     /* all-NaN draft: the exact path handles it */
+        if (tid == 0) A.exact[f] = 1;
+        return;
+    }
+    /* staged troughs [base, base + ns): all of them (global order), or the
+     * chunk's plus every segment its windows touch (+1 for segment ends) */
+    auto seg_of_g = [&](int64_t x) -> int {         /* last trough <= x, over global memory */
+        int lo = 0, hi = m;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (raw[mid] <= x) lo = mid + 1; else hi = mid; }
+        return lo - 1;
+    };
+    int base = 0, ns = m;
+    if (local) {
+        auto qpos = [&](int j) -> int64_t { const int64_t t = raw[j]; return t < vf ? vf : (t > vl ? vl : t); };
+        int64_t s, e;
+        win_bounds(qpos(jc0), n, W, s, e);
+        const int ja = seg_of_g(s > t0 ? s : t0);
+        win_bounds(qpos(jc1 - 1), n, W, s, e);
+        const int jb = seg_of_g(e - 1);
+        base = min(ja, jc0);
+        const int top = min(m - 1, max(jb + 1, jc1 - 1));
+        ns = top - base + 1;
+        if (ns > DB_TRMAX) {                           /* windows too wide to stage: exact path */
+            if (tid == 0) A.exact[f] = 1;
+            return;
+        }
+    }
+    for (int j = tid; j < ns; j += DB_T) {
+        const int64_t t = raw[base + j];
+        s_tp[j] = (int32_t)t;
+        s_tv[j] = env[t];
+    }
+    __syncthreads();
+    /* staged accessors by trough index */
+    auto tp = [&](int j) -> int64_t { return s_tp[j - base]; };
+    auto tv = [&](int j) -> double { return s_tv[j - base]; };
+    auto seg_lo = [&](int j) -> double { return j + 1 < m ? fmin(tv(j), tv(j + 1)) : tv(j); };
+    auto seg_hi = [&](int j) -> double { return j + 1 < m ? fmax(tv(j), tv(j + 1)) : tv(j); };
     /* stable ranks by end value (ties by index): order lists for the walks.
      * Long recordings skip them (O(m^2)) and rank each window's few segments
      * in place instead (below). */
@@ -712,32 +767,15 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         s_olo[ra] = (int16_t)j;
         s_ohi[rb] = (int16_t)j;
     }
-    /* valid outputs (nobs >= min_periods) form one interval */
-    {
-        int vf = INT_MAX, vl = -1;
-        for (int64_t i = tid; i < n; i += DB_T) {
-            int64_t s, e;
-            win_bounds(i, n, W, s, e);
-            const int64_t lo = s > t0 ? s : t0;
-            if (e - lo >= A.min_periods && e > lo) { vf = min(vf, (int)i); vl = max(vl, (int)i); }
-        }
-        for (int o = 32; o > 0; o >>= 1) { vf = min(vf, __shfl_xor(vf, o)); vl = max(vl, __shfl_xor(vl, o)); }
-        if (lane_id() == 0) { atomicMin(&s_vf, vf); atomicMax(&s_vl, vl); }
-    }
     __syncthreads();
-    const int vf = s_vf, vl = s_vl;
-    if (vl < vf) {                                     /* all-NaN draft: the exact path handles it */
-        if (tid == 0) A.exact[f] = 1;
-        return;
-    }
-    auto seg_of = [&](int64_t x) -> int {           /* last trough <= x (x >= t0) */
-        int lo = 0, hi = m;
-        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= x) lo = mid + 1; else hi = mid; }
+    auto seg_of = [&](int64_t x) -> int {           /* last trough <= x (x >= t0), among the staged */
+        int lo = base, hi = base + ns;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (tp(mid) <= x) lo = mid + 1; else hi = mid; }
         return lo - 1;
     };
     bool any_undecided = false;
     for (int j = jc0 + tid; j < jc1; j += DB_T) {
-        const int64_t t = s_tp[j];
+        const int64_t t = tp(j);
         const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
         int64_t s, e;
         win_bounds(qp, n, W, s, e);
@@ -748,8 +786,8 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         if (thr_u > nobs) thr_u = nobs;
         const int jl = seg_of(lo), jh = seg_of(hi - 1);
         auto len_of = [&](int i) -> int64_t {          /* samples of segment i inside [lo, hi) */
-            const int64_t a = lo > s_tp[i] ? lo : s_tp[i];
-            const int64_t se = i + 1 < m ? (int64_t)s_tp[i + 1] : n;
+            const int64_t a = lo > tp(i) ? lo : tp(i);
+            const int64_t se = i + 1 < m ? tp(i + 1) : n;
             return (hi < se ? hi : se) - a;
         };
         /* L: first lower end (ascending) whose in-window cumulative length exceeds k;
@@ -789,7 +827,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
                 if (ch >= thr_u) U = fmin(U, hb);
             }
         }
-        const double et = s_tv[j];
+        const double et = tv(j);
         uint8_t dcs;
         if (et <= A.mult * L) dcs = 1;
         else if (et > A.mult * U * (1.0 + 0x1p-50)) dcs = 0;

@@ -515,12 +515,13 @@ def test_longest_first_order_is_transparent(det):
             _check_file(ra, g)
 
 
-@pytest.mark.parametrize("secs", [0, 420])
+@pytest.mark.parametrize("secs", [0, 420, 1500])
 def test_draft_bounds_window_ranking(det, secs):
     """k_draft_bounds ranks each window's segments in place for recordings of
     > 512 troughs; the recording-wide order (BPMX_OPT_DRAFT_GLOBAL_RANK) and the
     full draft give the same floor, troughs and peaks (vulpine: 1456 raw
-    troughs; a 7-min recording: ~1700), and the oracle agrees."""
+    troughs; a 7-min recording: ~1700; a 25-min one: ~6000, staged per chunk),
+    and the oracle agrees."""
     from bpm_analysis_amd import _native as N
     if secs == 0:
         g = G.load("vulpine")
