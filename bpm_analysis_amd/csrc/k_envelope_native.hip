@@ -647,6 +647,158 @@ template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, co
 template __global__ void k_native_blocks_mfma<5>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 
 /* ---------------------------------------------------------------------- */
+/* int16 mono or stereo beyond k_native_blocks_mfma's K <= 160: the same exact
+ * integer GEMM with K = channels x (ds + 1) up to 32 KS.
+ *
+ * Stereo enters the K dimension as it lies in memory (L0 R0 L1 R1 ...), each
+ * coefficient digit duplicated for the two channels, so one accumulation
+ * gives sum_i q_i (L_i + R_i) exactly; the channel mean (bpm_analysis.py:1016,
+ * an exact f64 halving) is applied after the one rounding.  The coefficient
+ * fragments stay in registers for the whole kernel: one A fragment per M tile
+ * and K step serves both halves of the sample split (the high-byte products
+ * go to their own accumulators and shift by one digit row when the rows are
+ * combined), 8 KS registers.  With K up to 608, |acc| < 2^25, so the digit
+ * rows combine in f64 (exact below 2^53) rather than int32.
+ *
+ * One four-wave workgroup per CU (launch_bounds(256, 1): the fragments need
+ * the registers), one LDS-DMA slot of up to 38 KB per wave: tiles of up to 64
+ * blocks (mono) or 32 (stereo at ds = 300). */
+constexpr int NB_WAVES = 4;
+inline int nb_ndma() {                                  /* host: DMA wave-instructions per tile (1 KiB each) */
+    const int n = (160 * 1024 - ET_SIZE * 8 - 4 * 64 - 1024) / (NB_WAVES * 1024);
+    return n < 38 ? n : 38;
+}
+__host__ __device__ inline int nb_tile_blocks(int ds, int ch, int ks, int ndma) {
+    const int hw = ndma * 64 * 8;                        /* halfwords per slot */
+    const int b = (hw - 7 - 32 * ks - 2) / (ds * ch) + 1;
+    return b < 64 ? b : 64;
+}
+
+template <int KS>
+__global__ __launch_bounds__(64 * NB_WAVES, 1) void k_native_blocks_mfma_big(NatBlockArgs A, const nm_i4 *__restrict__ afrag,
+                                                                          const nm_i16 *__restrict__ ainit,
+                                                                          const double *__restrict__ cscale, int ndma) {
+    typedef nat_u4 u4;
+    extern __shared__ __align__(16) unsigned char nb_smem[];
+    __shared__ double s_et[ET_SIZE];
+    __shared__ nm_i16 s_init[4];
+    nat_stage_epilogue_tables(A, s_et);
+    for (int i = threadIdx.x; i < 4; i += blockDim.x) s_init[i] = ainit[(i >> 1) * 64 + (i & 1) * 32];
+    const int lane = lane_id(), hf = lane >> 5, wv = __builtin_amdgcn_readfirstlane(wave_id());
+    const int16_t *pcm = (const int16_t *)A.pcm;
+    const int64_t total = A.total;                        /* int16 elements */
+    const int ds = A.ds, bt = A.bt, ch = A.channels, bstride = ds * ch;
+    const int slot_ch = ndma * 64;
+    u4 *slot = (u4 *)nb_smem + wv * slot_ch;
+    const int nch = (7 + bt * bstride + ch + 7) >> 3;    /* chunks a tile may touch */
+    nm_i4 af[2][KS];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) af[t][s] = afrag[(t * KS + s) * 64 + lane];
+    double sc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sc[q] = cscale[2 * q + hf] * (ch == 2 ? 0.5 : 1.0);   /* exact */
+    __syncthreads();
+    const int64_t clast = (total & ~(int64_t)7) - 8;
+    auto dma = [&](int64_t e0) {
+        const int64_t a0 = e0 & ~(int64_t)7;
+        for (int r = 0; r < ndma; ++r) {
+            const int q = r * 64 + lane;
+            int64_t c = a0 + (int64_t)q * 8;
+            c = (q < nch && c + 8 <= total) ? c : clast;
+            const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(slot + r * 64);
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                         :: "v"(pcm + c), "s"(m0) : "memory");
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * NB_WAVES;
+    int64_t t = (int64_t)blockIdx.x * NB_WAVES + wv;
+    NatTile tl{};
+    if (t < A.n_tiles) {
+        tl = nat_tile_ld(A.tiles, t);
+        dma(tl.s0 * ch);
+    }
+    for (; t < A.n_tiles; t += stride) {
+        const int64_t tr = t + stride;
+        NatTile tn{};
+        if (tr < A.n_tiles) tn = nat_tile_ld(A.tiles, tr);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int64_t e0 = tl.s0 * ch;
+        const int coff = (int)(e0 & 7);
+        {
+            const int64_t a0 = e0 - coff, tail0 = total & ~(int64_t)7;
+            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))   /* last tile of the batch */
+                ((int16_t *)slot)[tail0 - a0 + lane] = pcm[tail0 + lane];
+            __builtin_amdgcn_wave_barrier();
+        }
+        const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
+        const uint32_t *tw = (const uint32_t *)slot;
+        double res[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            if (n == 1 && Lt <= 32) break;                   /* wave-uniform */
+            const int b = 32 * n + (lane & 31);
+            const int hw0 = coff + (b < Lt ? b : 0) * bstride + 16 * hf;
+            const uint32_t sh = (hw0 & 1) ? 16u : 0u;
+            nm_i16 l0 = s_init[hf], l1 = s_init[2 + hf];
+            nm_i16 h0 = {}, h1 = {};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const uint32_t *p = tw + ((hw0 + 32 * s) >> 1);
+                uint32_t w[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) w[i] = p[i];
+                nm_i4 bh, bl;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t e0w = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sh);
+                    const uint32_t e1w = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sh);
+                    bh[i] = (int32_t)__builtin_amdgcn_perm(e1w, e0w, 0x07050301u);
+                    bl[i] = (int32_t)(__builtin_amdgcn_perm(e1w, e0w, 0x06040200u) ^ 0x80808080u);
+                }
+                l0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s], bl, l0, 0, 0, 0);
+                l1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s], bl, l1, 0, 0, 0);
+                h0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s], bh, h0, 0, 0, 0);
+                h1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s], bh, h1, 0, 0, 0);
+            }
+            /* digit rows R_r = l_r + h_(r-1) (l: rows 0-3 in l0, 4-7 in l1) */
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double r0 = (double)l0[4 * q], r1 = (double)(l0[4 * q + 1] + h0[4 * q]);
+                const double r2 = (double)(l0[4 * q + 2] + h0[4 * q + 1]), r3 = (double)(l0[4 * q + 3] + h0[4 * q + 2]);
+                const double r4 = (double)(l1[4 * q] + h0[4 * q + 3]), r5 = (double)(l1[4 * q + 1] + h1[4 * q]);
+                const double r6 = (double)(l1[4 * q + 2] + h1[4 * q + 1]), r7 = (double)(l1[4 * q + 3] + h1[4 * q + 2]);
+                const double L = __builtin_fma(r3, 16777216.0, __builtin_fma(r2, 65536.0, __builtin_fma(r1, 256.0, r0)));
+                const double H = __builtin_fma(r7, 16777216.0, __builtin_fma(r6, 65536.0, __builtin_fma(r5, 256.0, r4)));
+                res[n][q] = __builtin_fma(H, 4294967296.0, L) * sc[q];
+            }
+        }
+        const int j = tl.j0 + lane;
+        const bool valid = lane < bt && j < tl.nb;
+        double x0 = 0.0;
+        if (valid) {
+            const int16_t *fr = (const int16_t *)slot + coff + lane * bstride;
+            x0 = ch == 2 ? 0.5 * (double)((int)fr[0] + (int)fr[1]) : (double)fr[0];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the slot is read: refill it */
+        if (tr < A.n_tiles) dma(tn.s0 * ch);
+        double cf[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double other = __shfl_xor(hf ? res[0][q] : res[1][q], 32);
+            cf[2 * q] = hf ? other : res[0][q];
+            cf[2 * q + 1] = hf ? res[1][q] : other;
+        }
+        nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{cf[0], cf[1], cf[2], cf[3]}, V4{cf[4], cf[5], cf[6], cf[7]},
+                          x0);
+        tl = tn;
+    }
+}
+template __global__ void k_native_blocks_mfma_big<10>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *, int);
+template __global__ void k_native_blocks_mfma_big<19>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *, int);
+
+/* ---------------------------------------------------------------------- */
 /* int16 interleaved PCM (stereo; also mono beyond the matrix-core path's
  * ds + 1 <= 160), f64 VALU block projections fed by LDS-DMA.
  *
@@ -1383,6 +1535,62 @@ std::vector<int32_t> build_mfma(const std::vector<LD> &cl, int R, int KS) {
                 }
     return w;
 }
+
+/* tables for k_native_blocks_mfma_big: as build_mfma, K = CH x R with each
+ * coefficient repeated for the CH interleaved channels, and one A fragment
+ * per (M tile, K step) carrying digit rows 4t + i (the high-byte products
+ * are shifted by a row when the accumulators combine):
+ *   [0, 16) scale | [16, 16 + 2*64*16) initial accumulators | [t][K step][lane][4 words] */
+std::vector<int32_t> build_mfma_big(const std::vector<LD> &cl, int R, int KS, int CH) {
+    std::vector<int64_t> q((size_t)R * 8);
+    std::vector<double> scale(8);
+    for (int c = 0; c < 8; ++c) {
+        LD mx = 0;
+        for (int i = 0; i < R; ++i) mx = std::max(mx, fabsl(cl[(size_t)i * 8 + c]));
+        int e = 0;
+        if (mx > 0) frexpl(mx, &e);
+        scale[c] = ldexp(1.0, e - NM_P);
+        for (int i = 0; i < R; ++i) q[(size_t)i * 8 + c] = llroundl(ldexpl(cl[(size_t)i * 8 + c], NM_P - e));
+    }
+    std::vector<int8_t> d((size_t)R * 64, 0);
+    for (int i = 0; i < R * 8; ++i) {
+        int64_t v = q[i];
+        for (int r = 0; r < NM_D; ++r) {
+            int dg = (int)(v & 255);
+            if (dg >= 128) dg -= 256;
+            d[(size_t)i * 8 + r] = (int8_t)dg;
+            v = (v - dg) >> 8;
+        }
+    }
+    const int K = R * CH;
+    auto dig = [&](int k, int c, int r) -> int {
+        return (k < K && r >= 0 && r < 8) ? d[((size_t)(k / CH) * 8 + c) * 8 + r] : 0;
+    };
+    std::vector<int32_t> w(16 + 2 * 64 * 16 + (size_t)2 * KS * 64 * 4, 0);
+    std::memcpy(w.data(), scale.data(), 64);
+    int32_t *init = w.data() + 16;
+    for (int t = 0; t < 2; ++t)
+        for (int l = 0; l < 64; ++l)
+            for (int reg = 0; reg < 16; ++reg) {
+                const int c = 2 * (reg >> 2) + (l >> 5), r = 4 * t + (reg & 3);
+                int64_t sum = 0;
+                for (int k = 0; k < K; ++k) sum += dig(k, c, r);
+                init[(t * 64 + l) * 16 + reg] = (int32_t)(128 * sum);
+            }
+    int32_t *af = init + 2 * 64 * 16;
+    for (int t = 0; t < 2; ++t)
+        for (int st = 0; st < KS; ++st)
+            for (int l = 0; l < 64; ++l) {
+                const int rho = l & 31;
+                const int c = 2 * (rho >> 3) + ((rho >> 2) & 1), r = 4 * t + (rho & 3);
+                for (int j = 0; j < 16; ++j) {
+                    const int k = 32 * st + 16 * (l >> 5) + j;
+                    const uint32_t byte = (uint8_t)(int8_t)dig(k, c, r);
+                    af[((t * KS + st) * 64 + l) * 4 + j / 4] |= (int32_t)(byte << (8 * (j & 3)));
+                }
+            }
+    return w;
+}
 }  // namespace
 
 /* fused-Hilbert plans and their device tables, cached per (device, Nd, window) */
@@ -1434,26 +1642,41 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* matrix-core path: int16 mono, ds + 1 <= 160 (KS K steps of 32 samples) */
     const int mfma_ks = ds + 1 <= 96 ? 3 : (ds + 1 <= 160 ? 5 : 0);
     const bool aligned16 = ((uintptr_t)B->pcm & 15) == 0;
-    const bool use_mfma = mfma_ks && P->dtype == BPMX_DT_I16 && P->channels == 1 && aligned16 &&
-                          foff[F] >= 16 && !(P->options & BPMX_OPT_NATIVE_F64);
-    /* int16 stereo (and, on request, mono) through the LDS-DMA f64 kernel */
-    const bool use_dma = !use_mfma && P->dtype == BPMX_DT_I16 && aligned16 && foff[F] * P->channels >= 16 &&
+    const bool i16_fast = P->dtype == BPMX_DT_I16 && aligned16 && foff[F] * P->channels >= 16 &&
+                          !(P->options & (BPMX_OPT_NATIVE_F64 | BPMX_OPT_NATIVE_DMA));
+    const bool use_mfma = mfma_ks && i16_fast && P->channels == 1;
+    /* int16 mono beyond K = 160 and int16 stereo: the big-K matrix-core kernel
+     * (K = channels x (ds + 1) <= 608) */
+    const int kbig = P->channels * (ds + 1);
+    const int big_ks = kbig <= 320 ? 10 : (kbig <= 608 ? 19 : 0);
+    const int nbdma = nb_ndma();
+    const bool use_big = !use_mfma && i16_fast && big_ks && (P->channels == 1 || P->channels == 2) &&
+                         nb_tile_blocks(ds, P->channels, big_ks, nbdma) >= 1;
+    /* the rest of int16 stereo (and, on request, mono) through the LDS-DMA f64 kernel */
+    const bool use_dma = !use_mfma && !use_big && P->dtype == BPMX_DT_I16 && aligned16 && foff[F] * P->channels >= 16 &&
                          (P->channels == 2 || (P->channels == 1 && (P->options & BPMX_OPT_NATIVE_DMA))) &&
                          !(P->options & BPMX_OPT_NATIVE_F64) && nd_tile_blocks(ds, P->channels) >= 1;
     /* tiles of bt blocks: the LDS tile (slot) must hold the tile's samples */
     const int bt = use_mfma ? nm_tile_blocks(ds, mfma_ks)
-                            : (use_dma ? nd_tile_blocks(ds, P->channels) : std::min(64, (NB_RCH * 512 - 16) / ds));
-    std::vector<int64_t> key(16);
+                 : use_big  ? nb_tile_blocks(ds, P->channels, big_ks, nbdma)
+                 : (use_dma ? nd_tile_blocks(ds, P->channels) : std::min(64, (NB_RCH * 512 - 16) / ds));
+    std::vector<int64_t> key(17);
     for (int i = 0; i < 12; ++i) std::memcpy(&key[i], &P->sos[i], 8);
     key[12] = ds;
     std::memcpy(&key[13], &P->sos_zi[0], 8);
     std::memcpy(&key[14], &P->sos_zi[2], 8);
     key[15] = bt;
+    key[16] = use_big ? 1000 * P->channels + big_ks : 0;
     size_t mfma_off = 0;                                     /* in doubles, into nat_tab */
     if (key != ctx->nat_key) {
         std::vector<LD> cl((size_t)(ds + 1) * 8);
         ctx->nat_tab = build_tables(P->sos, P->sos_zi, ds, bt, &cl);
-        if (mfma_ks) {
+        if (use_big) {
+            const std::vector<int32_t> w = build_mfma_big(cl, ds + 1, big_ks, P->channels);
+            const size_t o = ctx->nat_tab.size();
+            ctx->nat_tab.resize(o + w.size() / 2);
+            std::memcpy(ctx->nat_tab.data() + o, w.data(), w.size() * 4);
+        } else if (mfma_ks) {
             const std::vector<int32_t> w = build_mfma(cl, ds + 1, mfma_ks);
             const size_t o = ctx->nat_tab.size();
             ctx->nat_tab.resize(o + w.size() / 2);
@@ -1534,6 +1757,24 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             else
                 LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma<5>, dim3(g1), dim3(64 * NM_WAVES), 0, s, a, af,
                        init, mt);
+        } else if (use_big) {
+            a.total = foff[F] * P->channels;                 /* int16 elements */
+            const double *mt = d_tab + mfma_off;
+            const nm_i16 *init = (const nm_i16 *)(mt + 8);
+            const nm_i4 *af = (const nm_i4 *)(mt + 8 + 2 * 64 * 16 / 2);
+            const unsigned g1 = (unsigned)std::min<int64_t>((nt + NB_WAVES - 1) / NB_WAVES, 256);
+            const size_t lds = (size_t)nbdma * NB_WAVES * 1024;
+            if (big_ks == 10) {
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<10>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma_big<10>, dim3(g1), dim3(64 * NB_WAVES), lds, s,
+                       a, af, init, mt, nbdma);
+            } else {
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<19>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma_big<19>, dim3(g1), dim3(64 * NB_WAVES), lds, s,
+                       a, af, init, mt, nbdma);
+            }
         } else if (use_dma) {
             a.total = foff[F] * P->channels;                 /* int16 elements */
             const unsigned g1 = (unsigned)std::min<int64_t>((nt + ND_WAVES - 1) / ND_WAVES, 256);

@@ -684,13 +684,16 @@ def test_native_large_decimation(det, fs, ds_param, ch):
         _check_file(h, o, exact_env=False)
 
 
-@pytest.mark.parametrize("fs,ch,opt", [(96000, 2, 0), (48000, 2, 0), (44100, 2, 0), (96000, 1, 128)])
+@pytest.mark.parametrize("fs,ch,opt", [(96000, 2, 0), (48000, 2, 0), (44100, 2, 0), (96000, 1, 0), (192000, 1, 0),
+                                      (192000, 2, 0), (96000, 2, 128), (44100, 2, 128), (96000, 1, 128)])
 def test_native_dma_block_kernel(det, fs, ch, opt):
-    """The LDS-DMA f64 block kernel (default for int16 stereo; BPMX_OPT_NATIVE_DMA
-    for mono) agrees with the f64 VALU kernels it replaces (BPMX_OPT_NATIVE_F64;
-    the stereo channel sum is halved once at the end, which is exact) and gives
-    the oracle's indices, on a ragged batch whose last recording ends on a
-    partial 16-byte chunk."""
+    """The block kernels for int16 beyond the K <= 160 mono matrix-core path:
+    the big-K matrix-core kernel (default for stereo up to ds = 303 and mono up
+    to ds = 607: K = channels x (ds + 1) <= 608, the channels' products
+    accumulated exactly and halved once) and the LDS-DMA f64 kernel (beyond
+    that, e.g. 192 kHz stereo, or BPMX_OPT_NATIVE_DMA) agree with the f64 VALU
+    kernels (BPMX_OPT_NATIVE_F64) and give the oracle's indices, on a ragged
+    batch whose last recording ends on a partial 16-byte chunk."""
     import torch
     from bpm_analysis_amd import _native as N
     lens = [fs * 9 + 77, fs * 4, fs * 6 + 3]
