@@ -183,6 +183,106 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
     __syncthreads();
 }
 
+/* The same odd-prime stage as a GEMM on the matrix cores: nbf = M / p
+ * butterflies, butterfly (blk, n2) holding x_n at blk B + n2 + n L.  After the
+ * (a_n, b_n) pre-pass (with the DIT's conjugate twiddles first) the
+ * pair-symmetric DFT is four real products over n = 1..h:
+ *   Are = sum a_n.re c_nk,  Aim = sum a_n.im c_nk,  Bre = sum b_n.re s_nk,  Bim = sum b_n.im s_nk
+ * with c_nk, s_nk = cos, sin(2 pi (n k mod p) / p) from the exact table, i.e.
+ * [butterflies x n] x [n x k] GEMMs: v_mfma_f64_16x16x4_f64 (A: lane l = row
+ * l & 15, k-index l >> 4; B: k-index l >> 4, column l & 15; D: column l & 15,
+ * row (l >> 4) + 4 reg).  One 16-B LDS read each of a_n, b_n and (c, s) feeds
+ * the four MFMAs of a K step.  A wave owns HB_MF_UNITS (16 butterflies x 16
+ * frequencies) output tiles; results stay in registers until every wave has
+ * read, then the DIF twiddles are applied on the way out. */
+typedef double hb_d4 __attribute__((ext_vector_type(4)));
+template <bool INV, bool CONTIG>
+__device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int B, int Lr, int p, const double2 *ct) {
+    const int L = CONTIG ? 1 : Lr;                             /* contiguous stage: no index divisions */
+    const int h = (p - 1) >> 1, nbf = M / p, step = N / B;
+    for (int t = threadIdx.x; t < nbf * h; t += HB_T) {
+        const int bf = t / h, n = t - bf * h + 1;
+        const int blk = CONTIG ? bf : bf / L, n2 = CONTIG ? 0 : bf - blk * L, base = CONTIG ? bf * p : blk * B + n2;
+        double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
+        if (INV && n2) {
+            u = cmulc(u, S.tw(step * n2 * n));
+            v = cmulc(v, S.tw(step * n2 * (p - n)));
+        }
+        S.x[base + n * L] = cadd(u, v);
+        S.x[base + (p - n) * L] = csub(u, v);
+    }
+    __syncthreads();
+    const int ntl = (h + 16) >> 4, ks = (h + 3) >> 2, units = ((nbf + 15) >> 4) * ntl;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
+    auto base_of = [&](int bf) {
+        if (CONTIG) return bf * p;
+        const int blk = bf / L;
+        return blk * B + (bf - blk * L);
+    };
+    hb_d4 acc[HB_MF_UNITS][4];
+    double2 x0[HB_MF_UNITS][4];
+#pragma unroll
+    for (int u = 0; u < HB_MF_UNITS; ++u) {
+        const int unit = wv + u * (HB_T / 64);
+        if (unit < units) {                                    /* wave-uniform */
+            const int m = unit / ntl, nt = unit - m * ntl;
+            const int dA = 16 * m + r16, kB = 16 * nt + r16;
+            const bool rowok = dA < nbf;
+            const double2 *xa = S.x + base_of(rowok ? dA : 0);
+            hb_d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0, c2 = c0, c3 = c0;
+            int idx = ((kq + 1) * kB) % p;                     /* (n k) mod p, n = 4 s + kq + 1 */
+            const int st4 = (4 * kB) % p;
+            for (int s = 0; s < ks; ++s) {
+                const int n = 4 * s + kq + 1;
+                const bool ok = rowok && n <= h;
+                const double2 a = ok ? xa[n * L] : make_double2(0.0, 0.0);
+                const double2 b = ok ? xa[(p - n) * L] : make_double2(0.0, 0.0);
+                const double2 cs = ct[idx];
+                c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, cs.x, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, cs.x, c1, 0, 0, 0);
+                c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(b.x, cs.y, c2, 0, 0, 0);
+                c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(b.y, cs.y, c3, 0, 0, 0);
+                idx += st4;
+                if (idx >= p) idx -= p;
+            }
+            acc[u][0] = c0; acc[u][1] = c1; acc[u][2] = c2; acc[u][3] = c3;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * m + kq + 4 * r;
+                x0[u][r] = d < nbf ? S.x[base_of(d)] : make_double2(0.0, 0.0);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < HB_MF_UNITS; ++u) {
+        const int unit = wv + u * (HB_T / 64);
+        if (unit < units) {
+            const int m = unit / ntl, nt = unit - m * ntl, k = 16 * nt + r16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int d = 16 * m + kq + 4 * r;
+                if (d < nbf && k <= h) {
+                    const int blk = CONTIG ? d : d / L, n2 = CONTIG ? 0 : d - blk * L, base = CONTIG ? d * p : blk * B + n2;
+                    const double are = acc[u][0][r], aim = acc[u][1][r], bre = acc[u][2][r], bim = acc[u][3][r];
+                    const double2 xa = make_double2(x0[u][r].x + are, x0[u][r].y + aim);
+                    /* forward: X_k = x0 + A - iB, X_(p-k) = x0 + A + iB; inverse: signs swapped */
+                    const double2 mib = INV ? make_double2(-bim, bre) : make_double2(bim, -bre);
+                    const double2 r0 = cadd(xa, mib), r1 = csub(xa, mib);
+                    if (!INV && n2) {
+                        S.x[base + k * L] = k ? cmul(r0, S.tw(step * n2 * k)) : r0;
+                        if (k) S.x[base + (p - k) * L] = cmul(r1, S.tw(step * n2 * (p - k)));
+                    } else {
+                        S.x[base + k * L] = r0;
+                        if (k) S.x[base + (p - k) * L] = r1;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ int hb_pos(const HilbPlan &P, int k) {     /* position of frequency k after the DIF */
     int pos = 0;
     for (int i = 0; i < P.ns; ++i) {
@@ -212,6 +312,8 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     STAMP(0);
     for (int i = 0; i < P.ns; ++i) {
         if (P.rad[i] == 2) hb_radix2<false>(S, M, N, P.B[i], P.L[i]);
+        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<false, true>(S, M, N, P.B[i], 1, P.rad[i], S.pt + P.ptab[i]);
+        else if (P.mf[i]) hb_radixp_mfma<false, false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
         else hb_radixp<false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
         STAMP(i < 3 ? 1 + i : 3);
     }
@@ -237,6 +339,8 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     STAMP(4);
     for (int i = P.ns - 1; i >= 0; --i) {
         if (P.rad[i] == 2) hb_radix2<true>(S, M, N, P.B[i], P.L[i]);
+        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<true, true>(S, M, N, P.B[i], 1, P.rad[i], S.pt + P.ptab[i]);
+        else if (P.mf[i]) hb_radixp_mfma<true, false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
         else hb_radixp<true>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
     }
     STAMP(5);
@@ -295,7 +399,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
 
 /* ---------------------------------------------------------------------- */
 /* host: plan + tables (long double), cached per N */
-int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes) {
+int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes, bool mfma) {
     if (nd < 4 || (nd & 1)) return 0;
     const int64_t M = nd / 2;
     int rad[HB_MAXS], ns = 0;
@@ -328,8 +432,11 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
         P->L[i] = (int32_t)(B / r);
         B /= r;
         if (r > 2) {
+            /* matrix-core form: 16 x 16 output tiles within the waves' budget */
+            const int64_t units = ((M / r + 15) / 16) * (((r - 1) / 2 + 16) / 16);
+            P->mf[i] = mfma && r >= HB_MF_PMIN && units <= (int64_t)(HB_T / 64) * HB_MF_UNITS;
             /* register-held outputs: (M / p) ceil((h + 1) / HB_KB) tasks over HB_T threads */
-            if ((M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT) return 0;
+            if (!P->mf[i] && (M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT) return 0;
             int off = -1, acc = 0;
             for (int q : primes) { if (q == r) off = acc; acc += q; }
             if (off < 0) { off = acc; primes.push_back(r); }

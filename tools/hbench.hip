@@ -3,6 +3,8 @@
  * thread 0 of each workgroup): load | fwd stage 0 | 1 | 2 | pointwise | inverse | |z| | rolling mean.
  *   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/hbench.hip -o tools/hbench
  *   ./tools/hbench [files] [nd]
+ * Runs the plan with and without the matrix-core odd-prime stage and prints
+ * the largest envelope difference between the two (relative to max |env|).
  */
 #define BPMX_STAMPS 1
 #include "../bpm_analysis_amd/csrc/k_hilbert.hip"
@@ -13,19 +15,14 @@
 using namespace bpmx;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-int main(int argc, char **argv) {
-    const int F = argc > 1 ? atoi(argv[1]) : 1024;
-    const int64_t nd = argc > 2 ? atoll(argv[2]) : 18124;
+static double run(int F, int64_t nd, bool mfma, std::vector<double> &y, std::vector<double> &env_out) {
     HilbPlan P;
     std::vector<double2> tabs;
     size_t lds = 0;
-    if (!hilbert_plan(nd, 30, &P, &tabs, &lds)) { printf("no plan\n"); return 1; }
+    if (!hilbert_plan(nd, 30, &P, &tabs, &lds, mfma)) { printf("no plan\n"); exit(1); }
     printf("nd %lld M %d stages", (long long)nd, P.M);
-    for (int i = 0; i < P.ns; ++i) printf(" %d", P.rad[i]);
+    for (int i = 0; i < P.ns; ++i) printf(" %d%s", P.rad[i], P.mf[i] ? "(mfma)" : "");
     printf(" lds %zu\n", lds);
-    std::vector<double> y((size_t)F * nd);
-    unsigned long long s = 1;
-    for (auto &v : y) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (double)(s >> 11) / 9007199254740992.0 - 0.5; }
     std::vector<int64_t> doff(F + 1);
     for (int f = 0; f <= F; ++f) doff[f] = (int64_t)f * nd;
     std::vector<int32_t> act(F, 1);
@@ -43,6 +40,7 @@ int main(int argc, char **argv) {
     for (int it = 0; it < 3; ++it) hipLaunchKernelGGL(k_hilbert_env, dim3(F), dim3(HB_T), lds, 0, a, P);
     CK(hipDeviceSynchronize());
     const int R = 10;
+    CK(hipMemset(dst, 0, (size_t)F * 16 * 8));
     CK(hipEventRecord(e0));
     for (int it = 0; it < R; ++it) hipLaunchKernelGGL(k_hilbert_env, dim3(F), dim3(HB_T), lds, 0, a, P);
     CK(hipEventRecord(e1));
@@ -51,6 +49,8 @@ int main(int argc, char **argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     std::vector<unsigned long long> st((size_t)F * 16);
     CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
+    env_out.resize(y.size());
+    CK(hipMemcpy(env_out.data(), denv, y.size() * 8, hipMemcpyDeviceToHost));
     double acc[8] = {0};
     for (int f = 0; f < F; ++f) for (int k = 0; k < 8; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
     printf("kernel %.4f ms;  mean cycles per workgroup (s_memtime):", ms / R);
@@ -59,5 +59,21 @@ int main(int argc, char **argv) {
     for (int k = 0; k < 8; ++k) tot += acc[k] / F;
     for (int k = 0; k < 8; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
     printf("\n");
+    CK(hipFree(dy)); CK(hipFree(denv)); CK(hipFree(dd)); CK(hipFree(da)); CK(hipFree(dt)); CK(hipFree(dst));
+    return ms / R;
+}
+
+int main(int argc, char **argv) {
+    const int F = argc > 1 ? atoi(argv[1]) : 1024;
+    const int64_t nd = argc > 2 ? atoll(argv[2]) : 18124;
+    std::vector<double> y((size_t)F * nd);
+    unsigned long long s = 1;
+    for (auto &v : y) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (double)(s >> 11) / 9007199254740992.0 - 0.5; }
+    std::vector<double> e0, e1;
+    run(F, nd, false, y, e0);
+    run(F, nd, true, y, e1);
+    double mx = 0, d = 0;
+    for (size_t i = 0; i < e0.size(); ++i) { mx = fmax(mx, fabs(e0[i])); d = fmax(d, fabs(e0[i] - e1[i])); }
+    printf("max |env_direct - env_mfma| / max|env| = %.3e\n", d / mx);
     return 0;
 }
