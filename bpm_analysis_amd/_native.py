@@ -30,6 +30,7 @@ OPT_ROLLQ_GLOBAL = 64
 OPT_NATIVE_DMA = 128
 OPT_PEAKS_GLOBAL = 256
 OPT_HILBERT_R2C = 512
+OPT_REF_SERIAL_MEAN = 1024
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",

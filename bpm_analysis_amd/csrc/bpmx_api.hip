@@ -310,6 +310,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             std::memcpy(a.a, P->ba_a, sizeof a.a);
             std::memcpy(a.zi, P->ba_zi, sizeof a.zi);
             a.scratch = scr; a.env = O->env; a.y = O->y;
+            /* chain mode (the rolling mean's outputs formed in parallel afterwards) */
+            const bool chain = !(P->options & BPMX_OPT_REF_SERIAL_MEAN) && P->env_window > 1;
+            a.sums = chain ? (double *)ctx->buf("ref_sums", (size_t)std::max<int64_t>(maxnd, 1) * F * 8, &rc) : nullptr;
+            a.chain = (int32_t *)ctx->buf("ref_chain", (size_t)F * 4, &rc);
+            if (rc != BPMX_OK) return rc;
             const bool multi = P->channels > 1;
             const dim3 g((F + 63) / 64), b(64);
 #define ENV_REF(DT)                                                                                  \
@@ -323,6 +328,9 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             default: ENV_REF(BPMX_DT_F64) break;
             }
 #undef ENV_REF
+            if (chain)
+                LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean, dim3((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64)),
+                       dim3(64), 0, s, a);
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
             if (r != BPMX_OK) return r;

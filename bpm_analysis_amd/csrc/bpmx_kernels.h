@@ -21,7 +21,10 @@ struct EnvRefArgs {
     double *scratch;       /* interleaved [(maxNd+30) * F] */
     double *env;           /* [sumNd] */
     double *y;             /* [sumNd] or null */
+    double *sums;          /* interleaved [maxNd * F]: the rolling sum after each step (chain mode), or null */
+    int32_t *chain;        /* [F]: 1 = env left to k_ref_env_mean (chain mode), 0 = written in the pass */
 };
+__global__ void k_ref_env_mean(EnvRefArgs A);
 
 struct QuantArgs {
     const double *env;

@@ -20,6 +20,14 @@
  *    instruction instead of 64 scattered 8-B stores.
  * Roofline: the f64 dependency chain (~3 dependent ops per step, ~17 ops
  * issued per step by one wave) — neither HBM nor VALU throughput.
+ *
+ * The rolling mean splits into its chain and the rest ("chain mode", waves
+ * whose |y| has no NaN): only the Kahan add/remove recursion on sum_x is
+ * sequential, so the pass keeps just that (8 f64 ops per step, the running sum
+ * stored per step), and k_ref_env_mean forms every output in parallel from
+ * it — nobs from the window bounds, the run of equal added values and the
+ * last added value from |y| itself, then calc_mean's division and tests with
+ * the same rounded operations (pandas aggregations.pyx roll_mean).
  */
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
@@ -176,6 +184,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     /* wave-uniform trip counts (ragged files: lanes past their end are masked) */
     int64_t ndmax = nd;
     for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmax, o); ndmax = t > ndmax ? t : ndmax; }
+    if (have && A.chain) A.chain[f] = 0;
     if (ndmax == 0) return;
     /* shortest running file of the wave: blocks below it need no per-step
      * predicate, so a block's steps form one basic block the scheduler can
@@ -230,6 +239,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         }
     }
     /* ---------------- backward pass, in place ---------------- */
+    bool nanseen = false;
     {
         const int64_t ne = nd + 30;
         const int64_t nemax = ndmax + 30;
@@ -249,12 +259,20 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
             if (r0 + PFB <= ndmin + 30) {
                 if (run) {
 #pragma unroll
-                    for (int u = 0; u < PFB; ++u) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
+                    for (int u = 0; u < PFB; ++u) {
+                        const double yv = D.step(cur[u]);
+                        nanseen |= yv != yv;
+                        scr[(ne - 1 - r0 - u) * S] = yv;
+                    }
                 }
             } else if (run) {
 #pragma unroll
                 for (int u = 0; u < PFB; ++u)
-                    if (r0 + u < ne) scr[(ne - 1 - r0 - u) * S] = D.step(cur[u]);
+                    if (r0 + u < ne) {
+                        const double yv = D.step(cur[u]);
+                        nanseen |= yv != yv;
+                        scr[(ne - 1 - r0 - u) * S] = yv;
+                    }
             }
 #pragma unroll
             for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
@@ -277,6 +295,54 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         if (run) {
             R.prev = ldy(0);
             for (int64_t j = 0; j < e0; ++j) R.add(ldy(j));
+        }
+        const bool chain = A.sums && w > 1 && !__ballot(nanseen);   /* wave-uniform */
+        if (have && A.chain) A.chain[f] = chain && run ? 1 : 0;
+        if (chain) {
+            /* only the Kahan recursion; k_ref_env_mean forms the means */
+            double *__restrict__ sums = A.sums + (have ? f : 0);
+            double ca[PF], cr[PF], na[PF], nr[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u) { ca[u] = ldy(u + off); cr[u] = ldy(u + off - w); }
+            for (int64_t i0 = 0; i0 < ndmax; i0 += PF) {
+#pragma unroll
+                for (int u = 0; u < PF; ++u) {
+                    const int64_t i = i0 + PF + u;
+                    na[u] = ldy(i + off);
+                    nr[u] = ldy(i + off - w);
+                }
+                if (i0 >= w - off && i0 + PF + off <= ndmin) {
+                    /* steady state, no NaN in the wave: pandas remove_mean / add_mean's sum_x updates */
+                    double sum = R.sum, cad = R.cadd, crm = R.crem;
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) {
+                        const double yr = -cr[u] - crm, tr = sum + yr;
+                        crm = (tr - sum) - yr;
+                        sum = tr;
+                        const double ya = ca[u] - cad, ta = sum + ya;
+                        cad = (ta - sum) - ya;
+                        sum = ta;
+                        if (run) sums[(i0 + u) * S] = sum;
+                    }
+                    R.sum = sum; R.cadd = cad; R.crem = crm;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) {
+                        const int64_t i = i0 + u;
+                        if (run && i < nd) {
+                            if (i > 0) {
+                                const int64_t s = i + 1 + off - w;
+                                if (s > 0 && s <= nd) R.remove(cr[u]);
+                                if (i + off < nd) R.add(ca[u]);
+                            }
+                            sums[i * S] = R.sum;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < PF; ++u) { ca[u] = na[u]; cr[u] = nr[u]; }
+            }
+            return;
         }
         double ca[PF], cr[PF], na[PF], nr[PF], cy[PF], ny[PF];
 #pragma unroll
@@ -332,6 +398,60 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
             }
 #pragma unroll
             for (int u = 0; u < PF; ++u) { ca[u] = na[u]; cr[u] = nr[u]; cy[u] = ny[u]; }
+        }
+    }
+}
+
+/* chain mode's outputs: env[i] = calc_mean(minp 1, nobs, neg, sum_x, same,
+ * prev) for every (recording, step) in parallel.  In chain mode |y| has no
+ * NaN, so nobs is the clipped window length and neg is 0 (|y| never has its
+ * sign bit set); the last added value is |y[min(i + off, n - 1)]| and the run
+ * of equal added values ending there is counted back (it only matters up to
+ * nobs).  A tile of 64 steps x 64 recordings, transposed through LDS so the
+ * stores are contiguous; the y output (when requested) rides along. */
+__global__ __launch_bounds__(64) void k_ref_env_mean(EnvRefArgs A) {
+    __shared__ double st_env[STG][65];
+    __shared__ double st_y[STG][65];
+    const int lane = threadIdx.x;
+    const int f = blockIdx.y * 64 + lane;
+    const bool have = f < A.n_files;
+    const bool mine = have && A.chain[f];
+    const int64_t nd = have ? A.doff[f + 1] - A.doff[f] : 0;
+    const int64_t d0 = have ? A.doff[f] : 0;
+    const int64_t S = A.n_files, w = A.env_window, off = (w - 1) / 2;
+    const int64_t i00 = (int64_t)blockIdx.x * STG;
+    if (!__ballot(mine && i00 < nd)) return;
+    const double *__restrict__ y = A.scratch + 15 * S + (have ? f : 0);
+    const double *__restrict__ sums = A.sums + (have ? f : 0);
+    for (int r = 0; r < STG; ++r) {
+        const int64_t i = i00 + r;
+        double ev = 0.0, yv = 0.0;
+        if (mine && i < nd) {
+            int64_t s, e;
+            win_bounds(i, nd, w, s, e);
+            const int64_t nobs = e - s;
+            const int64_t a = i + off < nd - 1 ? i + off : nd - 1;   /* last added index */
+            const double prev = fabs(y[a * S]);
+            int64_t same = 1;
+            for (int64_t j = a - 1; j >= 0 && same < nobs && fabs(y[j * S]) == prev; --j) ++same;
+            double res = A.sums ? sums[i * S] / (double)nobs : 0.0;
+            if (same >= nobs) res = prev;
+            else if (res < 0) res = 0.0;                 /* neg_ct == 0 and result < 0 */
+            ev = nobs >= 1 ? res : __builtin_nan("");
+            yv = y[i * S];
+        }
+        st_env[r][lane] = ev;
+        st_y[r][lane] = yv;
+    }
+    __syncthreads();
+    const int rows = STG;
+    for (int fl = 0; fl < 64; ++fl) {
+        if (!__shfl((int)mine, fl)) continue;
+        const int64_t fd0 = __shfl(d0, fl), fnd = __shfl(nd, fl);
+        const int64_t i = i00 + lane;
+        if (lane < rows && i < fnd) {
+            A.env[fd0 + i] = st_env[lane][fl];
+            if (A.y) A.y[fd0 + i] = st_y[lane][fl];
         }
     }
 }

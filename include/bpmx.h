@@ -90,9 +90,11 @@ enum bpmx_option {
                                     block kernel (default for int16 stereo) instead of the register-prefetch one */
     BPMX_OPT_PEAKS_GLOBAL = 256, /* find_peaks by sample walks over global memory (k_find_peaks) for every
                                     recording instead of the LDS-resident extrema (test/diagnostic) */
-    BPMX_OPT_HILBERT_R2C = 512   /* native mode, recordings outside the fused Hilbert kernel: one rocFFT
+    BPMX_OPT_HILBERT_R2C = 512,  /* native mode, recordings outside the fused Hilbert kernel: one rocFFT
                                     R2C/C2R plan per distinct length instead of the batched Bluestein
                                     transform (test/diagnostic) */
+    BPMX_OPT_REF_SERIAL_MEAN = 1024  /* reference mode: form the rolling mean's outputs inside the sequential
+                                        pass instead of from its running sums in parallel (test/diagnostic) */
 };
 
 typedef struct bpmx_ctx bpmx_ctx;

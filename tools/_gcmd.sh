@@ -1,5 +1,4 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 120 ./tools/hbench 1024 18124 > gpurun_out/hb.log 2>&1; rc=$?; cat gpurun_out/hb.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "hilbert or native_mode_golden or c3_scale or native_ragged" > gpurun_out/pt.log 2>&1; rc=$?; tail -15 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 20 --warmup 3 --no-cpu > gpurun_out/b.log 2>&1; rc=$?; cut -c1-300 gpurun_out/b.log | tail -2; grep -o '"k_hilbert_env[^}]*}' gpurun_out/b.log; grep -o '"parity[^}]*}' gpurun_out/b.log; exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "reference or vulpine or synthetic_batch or ragged_batch_matches or dropin or c2 or c5_96k or stub or draft_bounds_window" > gpurun_out/pt.log 2>&1; rc=$?; tail -30 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 --mode reference --no-cpu > gpurun_out/br.log 2>&1; rc=$?; cut -c1-300 gpurun_out/br.log | tail -2; grep -o '"k_envelope_ref[^}]*}\|"k_ref_env_mean[^}]*}' gpurun_out/br.log; exit $rc
