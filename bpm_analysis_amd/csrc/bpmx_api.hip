@@ -301,7 +301,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     /* ---- ENVELOPE ---- */
     if (do_env) {
         if (P->mode == BPMX_MODE_REFERENCE) {
-            double *scr = (double *)ctx->buf("ref_scratch", (size_t)(maxnd + 30) * F * 8, &rc);
+            double *scr = (double *)ctx->buf("ref_scratch", (size_t)((maxnd + 30 + 63) / 64 * 64) * F * 8, &rc);
             if (rc != BPMX_OK) return rc;
             EnvRefArgs a;
             a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.active = d_active;
@@ -317,9 +317,15 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             if (rc != BPMX_OK) return rc;
             const bool multi = P->channels > 1;
             const dim3 g((F + 63) / 64), b(64);
+            const dim3 gp((unsigned)((maxnd + 30 + 63) / 64), (unsigned)((F + 63) / 64));
 #define ENV_REF(DT)                                                                                  \
-    if (multi) LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, true>), g, b, 0, s, a);         \
-    else LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, false>), g, b, 0, s, a);
+    if (multi) {                                                                                     \
+        LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, true>), gp, dim3(256), 0, s, a);                 \
+        LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, true>), g, b, 0, s, a);               \
+    } else {                                                                                         \
+        LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, false>), gp, dim3(256), 0, s, a);                \
+        LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, false>), g, b, 0, s, a);              \
+    }
             switch (P->dtype) {
             case BPMX_DT_U8: ENV_REF(BPMX_DT_U8) break;
             case BPMX_DT_I16: ENV_REF(BPMX_DT_I16) break;

@@ -23,6 +23,9 @@ struct EnvRefArgs {
     double *y;             /* [sumNd] or null */
     double *sums;          /* interleaved [maxNd * F]: the rolling sum after each step (chain mode), or null */
     int32_t *chain;        /* [F]: 1 = env left to k_ref_env_mean (chain mode), 0 = written in the pass */
+#ifdef BPMX_STAMPS
+    unsigned long long *stamps;
+#endif
 };
 __global__ void k_ref_env_mean(EnvRefArgs A);
 
@@ -211,6 +214,8 @@ constexpr int RQ_T = 256;   /* outputs per tile = threads per workgroup */
 
 template <int DT, bool MULTI>
 __global__ void k_envelope_ref_t(EnvRefArgs A);
+template <int DT, bool MULTI>
+__global__ void k_ref_pick(EnvRefArgs A);
 __global__ void k_quantile(QuantArgs A);
 __global__ void k_quantile_reg(QuantArgs A, BlockStatArgs B);
 __global__ void k_block_stats(BlockStatArgs A);

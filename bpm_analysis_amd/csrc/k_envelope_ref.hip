@@ -31,6 +31,7 @@
  */
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
+#include "bpmx_stamps.h"
 
 namespace bpmx {
 
@@ -145,9 +146,12 @@ struct RollMean {
 };
 
 #ifndef BPMX_REF_PFB
-#define BPMX_REF_PFB 16
+#define BPMX_REF_PFB 64
 #endif
-constexpr int PF = 16;   /* prefetch block (steps), rolling-mean phase */
+#ifndef BPMX_REF_PF
+#define BPMX_REF_PF 32
+#endif
+constexpr int PF = BPMX_REF_PF;   /* prefetch block (steps), rolling-mean phase */
 constexpr int PFB = BPMX_REF_PFB;   /* prefetch block of the two filter passes */
 constexpr int STG = 64;  /* LDS staging rows */
 
@@ -163,6 +167,43 @@ __device__ __forceinline__ void flush_rows(double (*stage)[65], double *__restri
     }
 }
 
+/* The odd-extended decimated input of filtfilt (x[::ds], 15 padded samples
+ * each side in the input dtype) gathered for every recording into the scratch
+ * rows [0, Nd + 30) that the forward pass then filters in place.  The stride-ds
+ * picks touch one cache line each; gathered here by many waves at once, with
+ * one recording's consecutive picks per wave (neighbouring pages), and
+ * transposed through LDS into [row][recording] rows, instead of inside the
+ * sequential pass, where 64 scattered picks per step (one per lane, 5 MB
+ * apart) cost ~440 cycles per step (tools/chainbench). */
+template <int DT, bool MULTI>
+__global__ __launch_bounds__(256) void k_ref_pick(EnvRefArgs A) {
+    __shared__ double tile[64][65];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * 64, f0 = (int64_t)blockIdx.y * 64;
+    const int64_t S = A.n_files, ds = A.ds;
+    const int ch = A.channels, wdt = work_dtype(DT, MULTI ? 2 : 1);
+    for (int fi = wv; fi < 64; fi += 4) {
+        const int64_t f = f0 + fi;
+        double v = 0.0;
+        if (f < S) {
+            const int64_t nd = A.doff[f + 1] - A.doff[f], r = r0 + lane;
+            if (nd > 15 && A.active[f] && r < nd + 30) {
+                const int64_t fb = A.foff[f], last = nd - 1;
+                auto xd = [&](int64_t j) { return frame_at<DT, MULTI>(A.pcm, ch, fb + j * ds); };
+                if (r < 15) v = odd_ext(wdt, xd(0), xd(15 - r));
+                else if (r < 15 + nd) v = xd(r - 15);
+                else v = odd_ext(wdt, xd(last), xd(last - 1 - (r - 15 - nd)));
+            }
+        }
+        tile[lane][fi] = v;
+    }
+    __syncthreads();
+    for (int ri = wv; ri < 64; ri += 4) {
+        const int64_t r = r0 + ri, f = f0 + lane;
+        if (f < S) A.scratch[r * S + f] = tile[ri][lane];
+    }
+}
+
 template <int DT, bool MULTI>
 __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     __shared__ double st_env[STG][65];
@@ -174,12 +215,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     const bool run = have && nd > 15 && A.active[f];
     if (!run) nd = 0;
     const int64_t d0 = have ? A.doff[f] : 0;
-    const int64_t fb = have ? A.foff[f] : 0;
-    const int64_t ds = A.ds;
-    const int ch = A.channels;
-    const int wdt = work_dtype(DT, MULTI ? 2 : 1);
     const int64_t S = A.n_files;
-    const void *__restrict__ pcm = A.pcm;
     double *__restrict__ scr = A.scratch + (have ? f : 0);
     /* wave-uniform trip counts (ragged files: lanes past their end are masked) */
     int64_t ndmax = nd;
@@ -197,72 +233,77 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     D.b0 = A.b[0]; D.b1 = A.b[1]; D.b2 = A.b[2]; D.b3 = A.b[3]; D.b4 = A.b[4];
     D.a1 = A.a[1]; D.a2 = A.a[2]; D.a3 = A.a[3]; D.a4 = A.a[4];
     const int64_t last = nd > 0 ? nd - 1 : 0;
-    auto xd = [&](int64_t j) -> double {
-        j = j < 0 ? 0 : (j > last ? last : j);
-        return frame_at<DT, MULTI>(pcm, ch, fb + j * ds);
-    };
+    STAMP_DECL
 
-    /* ---------------- forward pass ---------------- */
+    /* Row addresses: every lane walks its own column with a pointer that
+     * advances by PFB rows per block; inside blocks that no lane can run past
+     * (the common case) the offsets u * S are loop-invariant, so a load or a
+     * store is one instruction with no clamping or 64-bit index arithmetic. */
+    const int64_t SB = (int64_t)PFB * S;
+    const int64_t nemax = ndmax + 30;
+    /* lanes that do not run address a full-length column (they only load, never store) */
+    const int64_t ne = run ? nd + 30 : nemax;
+    const int64_t nemin = ndmin == INT64_MAX ? nemax : ndmin + 30;   /* shortest running column */
+    /* ---------------- forward pass, in place over the gathered rows ---------------- */
     {
-        double padv[15], padr[15];
-        const double x0 = xd(0), xl = xd(last);
-#pragma unroll
-        for (int k = 0; k < 15; ++k) { padv[k] = xd(15 - k); padr[k] = xd(last - 1 - k); }
+        auto ldc = [&](int64_t r) -> double { return scr[(r < ne ? r : ne - 1) * S]; };   /* clamped */
         double cur[PFB], nxt[PFB];
 #pragma unroll
-        for (int u = 0; u < PFB; ++u) cur[u] = xd(u);
-        if (run) {
-            const double e0 = odd_ext(wdt, x0, padv[0]);
-            D.init(A.zi, e0);
+        for (int u = 0; u < PFB; ++u) cur[u] = ldc(u);
+        if (run) D.init(A.zi, cur[0]);
+        double *p = scr;                                     /* row r0 */
+        for (int64_t r0 = 0; r0 < nemax; r0 += PFB, p += SB) {
+            if (r0 + 2 * PFB <= nemin) {
 #pragma unroll
-            for (int k = 0; k < 15; ++k) scr[k * S] = D.step(odd_ext(wdt, x0, padv[k]));
-        }
-        for (int64_t j0 = 0; j0 < ndmax; j0 += PFB) {
+                for (int u = 0; u < PFB; ++u) nxt[u] = p[SB + u * S];
+            } else {
 #pragma unroll
-            for (int u = 0; u < PFB; ++u) nxt[u] = xd(j0 + PFB + u);
-            if (j0 + PFB <= ndmin) {
+                for (int u = 0; u < PFB; ++u) nxt[u] = ldc(r0 + PFB + u);
+            }
+            if (r0 + PFB <= nemin) {
                 if (run) {
 #pragma unroll
-                    for (int u = 0; u < PFB; ++u) scr[(15 + j0 + u) * S] = D.step(cur[u]);
+                    for (int u = 0; u < PFB; ++u) p[u * S] = D.step(cur[u]);
                 }
             } else if (run) {
 #pragma unroll
                 for (int u = 0; u < PFB; ++u)
-                    if (j0 + u < nd) scr[(15 + j0 + u) * S] = D.step(cur[u]);
+                    if (r0 + u < ne) p[u * S] = D.step(cur[u]);
             }
 #pragma unroll
             for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
         }
-        if (run) {
-#pragma unroll
-            for (int k = 0; k < 15; ++k) scr[(15 + nd + k) * S] = D.step(odd_ext(wdt, xl, padr[k]));
-        }
     }
+    STAMP(0);
     /* ---------------- backward pass, in place ---------------- */
     bool nanseen = false;
     {
-        const int64_t ne = nd + 30;
-        const int64_t nemax = ndmax + 30;
-        /* lane-local reversed index r -> scratch row ne-1-r; lanes with r >= ne idle */
-        auto ld = [&](int64_t r) -> double {
+        /* reversed index r -> row ne - 1 - r (clamped at 0 past the column's start) */
+        auto ldc = [&](int64_t r) -> double {
             int64_t row = ne - 1 - r;
             row = row < 0 ? 0 : row;
             return scr[row * S];
         };
         double cur[PFB], nxt[PFB];
 #pragma unroll
-        for (int u = 0; u < PFB; ++u) cur[u] = ld(u);
+        for (int u = 0; u < PFB; ++u) cur[u] = ldc(u);
         if (run) D.init(A.zi, cur[0]);
-        for (int64_t r0 = 0; r0 < nemax; r0 += PFB) {
+        double *p = scr + (ne - 1) * S;                      /* row ne - 1 - r0 */
+        for (int64_t r0 = 0; r0 < nemax; r0 += PFB, p -= SB) {
+            if (r0 + 2 * PFB <= nemin) {
 #pragma unroll
-            for (int u = 0; u < PFB; ++u) nxt[u] = ld(r0 + PFB + u);
-            if (r0 + PFB <= ndmin + 30) {
+                for (int u = 0; u < PFB; ++u) nxt[u] = p[-SB - u * S];
+            } else {
+#pragma unroll
+                for (int u = 0; u < PFB; ++u) nxt[u] = ldc(r0 + PFB + u);
+            }
+            if (r0 + PFB <= nemin) {
                 if (run) {
 #pragma unroll
                     for (int u = 0; u < PFB; ++u) {
                         const double yv = D.step(cur[u]);
                         nanseen |= yv != yv;
-                        scr[(ne - 1 - r0 - u) * S] = yv;
+                        p[-u * S] = yv;
                     }
                 }
             } else if (run) {
@@ -271,13 +312,14 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                     if (r0 + u < ne) {
                         const double yv = D.step(cur[u]);
                         nanseen |= yv != yv;
-                        scr[(ne - 1 - r0 - u) * S] = yv;
+                        p[-u * S] = yv;
                     }
             }
 #pragma unroll
             for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
         }
     }
+    STAMP(1);
     /* ---------------- |y| centred rolling mean over rows [15, 15+nd) ---------------- */
     {
         const double *__restrict__ y = scr + 15 * S;
@@ -300,16 +342,23 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         if (have && A.chain) A.chain[f] = chain && run ? 1 : 0;
         if (chain) {
             /* only the Kahan recursion; k_ref_env_mean forms the means */
-            double *__restrict__ sums = A.sums + (have ? f : 0);
+            double *__restrict__ ps = A.sums + (have ? f : 0);          /* row i0 of the running sums */
+            const double *pa = y + off * S, *pr = y + (off - w) * S;   /* rows i0 + off, i0 + off - w */
+            const int64_t SP = (int64_t)PF * S;
             double ca[PF], cr[PF], na[PF], nr[PF];
 #pragma unroll
             for (int u = 0; u < PF; ++u) { ca[u] = ldy(u + off); cr[u] = ldy(u + off - w); }
-            for (int64_t i0 = 0; i0 < ndmax; i0 += PF) {
+            for (int64_t i0 = 0; i0 < ndmax; i0 += PF, ps += SP, pa += SP, pr += SP) {
+                if (i0 + PF + off - w >= 0 && i0 + 2 * PF + off <= ndmin) {
 #pragma unroll
-                for (int u = 0; u < PF; ++u) {
-                    const int64_t i = i0 + PF + u;
-                    na[u] = ldy(i + off);
-                    nr[u] = ldy(i + off - w);
+                    for (int u = 0; u < PF; ++u) { na[u] = fabs(pa[SP + u * S]); nr[u] = fabs(pr[SP + u * S]); }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < PF; ++u) {
+                        const int64_t i = i0 + PF + u;
+                        na[u] = ldy(i + off);
+                        nr[u] = ldy(i + off - w);
+                    }
                 }
                 if (i0 >= w - off && i0 + PF + off <= ndmin) {
                     /* steady state, no NaN in the wave: pandas remove_mean / add_mean's sum_x updates */
@@ -322,7 +371,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                         const double ya = ca[u] - cad, ta = sum + ya;
                         cad = (ta - sum) - ya;
                         sum = ta;
-                        if (run) sums[(i0 + u) * S] = sum;
+                        if (run) ps[u * S] = sum;
                     }
                     R.sum = sum; R.cadd = cad; R.crem = crm;
                 } else {
@@ -335,13 +384,15 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                                 if (s > 0 && s <= nd) R.remove(cr[u]);
                                 if (i + off < nd) R.add(ca[u]);
                             }
-                            sums[i * S] = R.sum;
+                            ps[u * S] = R.sum;
                         }
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < PF; ++u) { ca[u] = na[u]; cr[u] = nr[u]; }
             }
+            STAMP(2);
+            STAMP_FLUSH(A.stamps);
             return;
         }
         double ca[PF], cr[PF], na[PF], nr[PF], cy[PF], ny[PF];
@@ -456,6 +507,16 @@ __global__ __launch_bounds__(64) void k_ref_env_mean(EnvRefArgs A) {
     }
 }
 
+template __global__ void k_ref_pick<BPMX_DT_U8, false>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_I16, false>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_I32, false>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_F32, false>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_F64, false>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_U8, true>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_I16, true>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_I32, true>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_F32, true>(EnvRefArgs);
+template __global__ void k_ref_pick<BPMX_DT_F64, true>(EnvRefArgs);
 template __global__ void k_envelope_ref_t<BPMX_DT_U8, false>(EnvRefArgs);
 template __global__ void k_envelope_ref_t<BPMX_DT_I16, false>(EnvRefArgs);
 template __global__ void k_envelope_ref_t<BPMX_DT_I32, false>(EnvRefArgs);
