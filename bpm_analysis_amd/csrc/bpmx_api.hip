@@ -336,7 +336,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
 #undef ENV_REF
             if (chain)
                 LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean, dim3((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64)),
-                       dim3(64), 0, s, a);
+                       dim3(256), 0, s, a);
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
             if (r != BPMX_OK) return r;

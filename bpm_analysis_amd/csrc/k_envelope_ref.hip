@@ -460,10 +460,10 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
  * of equal added values ending there is counted back (it only matters up to
  * nobs).  A tile of 64 steps x 64 recordings, transposed through LDS so the
  * stores are contiguous; the y output (when requested) rides along. */
-__global__ __launch_bounds__(64) void k_ref_env_mean(EnvRefArgs A) {
+__global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
     __shared__ double st_env[STG][65];
     __shared__ double st_y[STG][65];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int f = blockIdx.y * 64 + lane;
     const bool have = f < A.n_files;
     const bool mine = have && A.chain[f];
@@ -471,36 +471,54 @@ __global__ __launch_bounds__(64) void k_ref_env_mean(EnvRefArgs A) {
     const int64_t d0 = have ? A.doff[f] : 0;
     const int64_t S = A.n_files, w = A.env_window, off = (w - 1) / 2;
     const int64_t i00 = (int64_t)blockIdx.x * STG;
-    if (!__ballot(mine && i00 < nd)) return;
+    if (!__syncthreads_or(mine && i00 < nd)) return;
     const double *__restrict__ y = A.scratch + 15 * S + (have ? f : 0);
     const double *__restrict__ sums = A.sums + (have ? f : 0);
-    for (int r = 0; r < STG; ++r) {
-        const int64_t i = i00 + r;
-        double ev = 0.0, yv = 0.0;
+    /* this wave's 16 rows: every load issued first, then the arithmetic */
+    constexpr int R = STG / 4;
+    const int64_t ib = i00 + wv * R;
+    const int64_t lastr = nd > 0 ? nd - 1 : 0;
+    double sm[R], ya[R], yb[R], yi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = ib + r;
+        const bool ok = mine && i < nd;
+        const int64_t ic = ok ? i : 0;
+        const int64_t a = ic + off < lastr ? ic + off : lastr;            /* last added index */
+        sm[r] = ok ? sums[ic * S] : 0.0;
+        ya[r] = ok ? y[a * S] : 0.0;
+        yb[r] = ok && a > 0 ? y[(a - 1) * S] : 0.0;
+        yi[r] = ok ? y[ic * S] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = ib + r;
+        double ev = 0.0;
         if (mine && i < nd) {
             int64_t s, e;
             win_bounds(i, nd, w, s, e);
             const int64_t nobs = e - s;
-            const int64_t a = i + off < nd - 1 ? i + off : nd - 1;   /* last added index */
-            const double prev = fabs(y[a * S]);
+            const int64_t a = i + off < lastr ? i + off : lastr;
+            const double prev = fabs(ya[r]);
             int64_t same = 1;
-            for (int64_t j = a - 1; j >= 0 && same < nobs && fabs(y[j * S]) == prev; --j) ++same;
-            double res = A.sums ? sums[i * S] / (double)nobs : 0.0;
+            if (a > 0 && same < nobs && fabs(yb[r]) == prev) {   /* rare: a run of equal values */
+                ++same;
+                for (int64_t j = a - 2; j >= 0 && same < nobs && fabs(y[j * S]) == prev; --j) ++same;
+            }
+            double res = sm[r] / (double)nobs;
             if (same >= nobs) res = prev;
             else if (res < 0) res = 0.0;                 /* neg_ct == 0 and result < 0 */
             ev = nobs >= 1 ? res : __builtin_nan("");
-            yv = y[i * S];
         }
-        st_env[r][lane] = ev;
-        st_y[r][lane] = yv;
+        st_env[wv * R + r][lane] = ev;
+        st_y[wv * R + r][lane] = yi[r];
     }
     __syncthreads();
-    const int rows = STG;
-    for (int fl = 0; fl < 64; ++fl) {
+    for (int fl = wv; fl < 64; fl += 4) {
         if (!__shfl((int)mine, fl)) continue;
         const int64_t fd0 = __shfl(d0, fl), fnd = __shfl(nd, fl);
         const int64_t i = i00 + lane;
-        if (lane < rows && i < fnd) {
+        if (i < fnd) {
             A.env[fd0 + i] = st_env[lane][fl];
             if (A.y) A.y[fd0 + i] = st_y[lane][fl];
         }

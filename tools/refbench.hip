@@ -48,7 +48,7 @@ int main(int argc, char **argv) {
         CK(hipEventRecord(e[1]));
         hipLaunchKernelGGL((k_envelope_ref_t<BPMX_DT_I16, false>), g, dim3(64), 0, 0, a);
         CK(hipEventRecord(e[2]));
-        hipLaunchKernelGGL(k_ref_env_mean, gm, dim3(64), 0, 0, a);
+        hipLaunchKernelGGL(k_ref_env_mean, gm, dim3(256), 0, 0, a);
         CK(hipEventRecord(e[3]));
         CK(hipEventSynchronize(e[3]));
     }
