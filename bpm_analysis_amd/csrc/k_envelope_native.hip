@@ -494,7 +494,10 @@ typedef int32_t nm_i16 __attribute__((ext_vector_type(16)));
  * the 160 KiB LDS, and with 8 waves interleaving, ~6 of the 8 tiles are in
  * flight at any time. */
 constexpr int NM_WAVES = 4;
-constexpr int NM_SLOTS = 1;                       /* LDS tile slots per wave */
+#ifndef BPMX_NM_SLOTS
+#define BPMX_NM_SLOTS 1
+#endif
+constexpr int NM_SLOTS = BPMX_NM_SLOTS;             /* LDS tile slots per wave */
 constexpr int NM_MINW = 2;                        /* waves per SIMD the register budget must allow */
 constexpr int NM_NDMA = 18;                      /* DMA wave-instructions per tile, always all issued, all lanes on */
 constexpr int NM_SLOT_CH = NM_NDMA * 64;          /* 16-byte chunks per slot (18,432 B) */
