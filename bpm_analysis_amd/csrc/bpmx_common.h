@@ -157,6 +157,19 @@ __device__ __forceinline__ int wave_shr1_dpp(int x, int edge) {
     return __builtin_amdgcn_update_dpp(edge, x, 0x138, 0xf, 0xf, false);   /* wave_shr:1 */
 }
 
+/* f64 one-lane wave shifts (DPP wave_shr:1 / wave_shl:1 on both halves): the
+ * lane below / above, `edge` at lane 0 / 63.  Every lane must be active. */
+__device__ __forceinline__ double dpp_shr1_d(double x, double edge) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_shl1_d(double x, double edge) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(x), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(x), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
 /* exclusive block scan of 0/1 flags; `sh` holds NT/64+1 ints.  Returns the
  * exclusive prefix, writes the block total to *total.  Ends with a barrier. */
 template <int NT>

@@ -656,16 +656,28 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     int32_t *mp_g = A.cand + d0, *vp_g = A.vcand + d0;
     int cm = 0, cv = 0;                                      /* wave-uniform counts */
     const unsigned long long lt = (1ull << lane) - 1ull;
+    /* one coalesced load per 64 positions, issued a block ahead; the left and
+     * right neighbours come from the adjacent lanes (DPP wave shifts), the
+     * block edges from the previous / next block's end lanes */
+    double xc = w0 < w1 && w0 + lane < n ? sg * e[w0 + lane] : 0.0;
+    double xedge = w0 < w1 ? sg * e[w0 - 1] : 0.0;           /* position b - 1 */
     for (int64_t b = w0; b < w1; b += 64) {
         const int64_t i = b + lane;
+        const double xn = b + 64 + lane < n ? sg * e[b + 64 + lane] : 0.0;
+        const double xl = dpp_shr1_d(xc, xedge);
+        const double xr1 = dpp_shl1_d(xc, __shfl(xn, 0));
         bool ism = false, isv = false;
         int32_t pk = 0;
         if (i < w1) {
-            const double xi = sg * e[i], xl = sg * e[i - 1];
+            const double xi = xc;
             if (xl != xi) {
                 int64_t ia = i + 1;
-                while (ia < n - 1 && sg * e[ia] == xi) ia++;
-                const double xr = sg * e[ia];
+                double xr = xr1;
+                if (xr == xi && ia < n - 1) {                    /* plateau: walk it */
+                    ia = i + 2;
+                    while (ia < n - 1 && sg * e[ia] == xi) ia++;
+                    xr = sg * e[ia];
+                }
                 if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
                 else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)i; }
             }
@@ -675,6 +687,8 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         if (isv) vp_g[w0 - 1 + cv + __popcll(bv & lt)] = pk;
         cm += __popcll(bm);
         cv += __popcll(bv);
+        xedge = __shfl(xc, 63);
+        xc = xn;
     }
     if (lane == 0) { s_gc[0][0][wid] = cm; s_gc[1][0][wid] = cv; }
     __syncthreads();

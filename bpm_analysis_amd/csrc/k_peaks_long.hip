@@ -54,16 +54,25 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_scan(PeakArgs A, FplArgs L) {
     int32_t *mp_g = A.cand + d0 + (int64_t)u * FPL_U, *vp_g = A.vcand + d0 + (int64_t)u * FPL_U;
     int cm = 0, cv = 0;
     const unsigned long long lt = (1ull << lane) - 1ull;
+    double xc = w0 + lane < n ? sg * e[w0 + lane] : 0.0;     /* as k_find_peaks_lds: one load a block ahead */
+    double xedge = sg * e[w0 - 1];
     for (int64_t b = w0; b < w1; b += 64) {
         const int64_t i = b + lane;
+        const double xn = b + 64 + lane < n ? sg * e[b + 64 + lane] : 0.0;
+        const double xl = dpp_shr1_d(xc, xedge);
+        const double xr1 = dpp_shl1_d(xc, __shfl(xn, 0));
         bool ism = false, isv = false;
         int32_t pk = 0;
         if (i < w1) {
-            const double xi = sg * e[i], xl = sg * e[i - 1];
+            const double xi = xc;
             if (xl != xi) {
                 int64_t ia = i + 1;
-                while (ia < n - 1 && sg * e[ia] == xi) ia++;
-                const double xr = sg * e[ia];
+                double xr = xr1;
+                if (xr == xi && ia < n - 1) {
+                    ia = i + 2;
+                    while (ia < n - 1 && sg * e[ia] == xi) ia++;
+                    xr = sg * e[ia];
+                }
                 if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
                 else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)i; }
             }
@@ -73,6 +82,8 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_scan(PeakArgs A, FplArgs L) {
         if (isv) vp_g[cv + __popcll(bv & lt)] = pk;
         cm += __popcll(bm);
         cv += __popcll(bv);
+        xedge = __shfl(xc, 63);
+        xc = xn;
     }
     if (lane == 0) {
         int32_t *c = L.cnt + ((int64_t)f * L.nu + u) * 2;
