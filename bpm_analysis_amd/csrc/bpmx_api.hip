@@ -405,6 +405,28 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         const int64_t gy = std::min<int64_t>((((maxnd + 63) >> 6) + 3) / 4, std::max<int64_t>(1, 2048 / F));
         LAUNCH(ctx, s, "k_block_stats", k_block_stats, dim3(F, (unsigned)gy), dim3(256), 0, s, bs);
     }
+    /* long recordings' quantiles: radix select over many workgroups (k_ql_*) */
+    auto quantile_long = [&](const QuantArgs &q) -> int {
+        int qrc = BPMX_OK;
+        QlArgs A;
+        A.Q = q;
+        A.st = (QlState *)ctx->buf("ql_state", (size_t)F * Q_SLOTS * sizeof(QlState), &qrc);
+        const size_t hb = (size_t)QL_PASSES * F * Q_SLOTS * QL_BINS * 4;
+        A.hist = (unsigned int *)ctx->buf("ql_hist", hb, &qrc);
+        if (qrc != BPMX_OK) return qrc;
+        HIP_TRY(hipMemsetAsync(A.hist, 0, hb, s));
+        const dim3 gc((unsigned)((maxnd + QL_CHUNK - 1) / QL_CHUNK), (unsigned)F);
+        A.pass = 0;
+        LAUNCH(ctx, s, "k_quantile", k_ql_init, dim3(F), dim3(64), 0, s, A);
+        for (int p = 0; p < QL_PASSES; ++p) {
+            A.pass = p;
+            LAUNCH(ctx, s, "k_quantile", k_ql_hist, gc, dim3(256), 0, s, A);
+            LAUNCH(ctx, s, "k_quantile", k_ql_select, dim3(F, q.n_levels), dim3(256), 0, s, A);
+        }
+        LAUNCH(ctx, s, "k_quantile", k_ql_next, gc, dim3(256), 0, s, A);
+        LAUNCH(ctx, s, "k_quantile", k_ql_final, dim3(F), dim3(64), 0, s, A);
+        return BPMX_OK;
+    };
     {
         QuantArgs a;
         a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
@@ -428,7 +450,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         a.skip = nullptr;
         a.stats = 0;                      /* k_find_peaks builds its own block tables when it runs */
         LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-        if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, L), dim3(1024), 0, s, a);
+        if (long_files && (rc = quantile_long(a)) != BPMX_OK) return rc;
     }
 
     /* ---- FLOOR ---- */
@@ -454,7 +476,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.n_levels = 1; a.q[0] = P->noise_floor_q; a.slot[0] = 1 << Q_NOISE;
             a.skip = d_run1; a.stats = 0;
             LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-            if (long_files) LAUNCH(ctx, s, "k_quantile", k_quantile, dim3(F, 1), dim3(1024), 0, s, a);
+            if (long_files && (rc = quantile_long(a)) != BPMX_OK) return rc;
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
         const int64_t W = bad_window ? P->min_periods : P->noise_window;

@@ -37,10 +37,34 @@ struct QuantArgs {
     int32_t slot[Q_SLOTS];  /* bitmask of the qv slots level l fills */
     double q[Q_SLOTS];
     double *qv;             /* [F][Q_SLOTS] */
-    int64_t skip_le;        /* k_quantile: files with n <= skip_le are done by k_quantile_reg */
+    int64_t skip_le;        /* k_ql_*: files with n <= skip_le are done by k_quantile_reg */
     const int32_t *skip;    /* [F] optional: skip files with skip[f] != 0 (the lazy static-floor level) */
     int32_t stats;          /* k_quantile_reg: also write the block max/min tables */
 };
+
+/* k_quantile for long recordings over many workgroups (k_detect.hip):
+ * MSD radix select with 11-bit digits (6 passes over the 64-bit keys), each
+ * pass a histogram of every chunk of the recording (all levels at once) into
+ * global bins, then a select step per (recording, level) */
+constexpr int QL_BITS = 11, QL_BINS = 1 << QL_BITS, QL_PASSES = 6, QL_CHUNK = 32768;
+struct QlState {
+    unsigned long long prefix, mask;
+    long long r;            /* rank still to find inside the selected bin */
+    long long lo;           /* the order statistic's rank (floor((n-1) q)) */
+    unsigned long long next; /* min key above the answer (atomicMin), for the interpolation */
+    int32_t top, eq;        /* top: q (n-1) >= n-1; eq: another key equals the answer */
+};
+struct QlArgs {
+    QuantArgs Q;
+    QlState *st;            /* [F][Q_SLOTS] */
+    unsigned int *hist;     /* [QL_PASSES][F][Q_SLOTS][QL_BINS] (zeroed before pass 0) */
+    int32_t pass;
+};
+__global__ void k_ql_init(QlArgs A);
+__global__ void k_ql_hist(QlArgs A);
+__global__ void k_ql_select(QlArgs A);
+__global__ void k_ql_next(QlArgs A);
+__global__ void k_ql_final(QlArgs A);
 
 struct BlockStatArgs {
     const double *env;
@@ -216,7 +240,6 @@ template <int DT, bool MULTI>
 __global__ void k_envelope_ref_t(EnvRefArgs A);
 template <int DT, bool MULTI>
 __global__ void k_ref_pick(EnvRefArgs A);
-__global__ void k_quantile(QuantArgs A);
 __global__ void k_quantile_reg(QuantArgs A, BlockStatArgs B);
 __global__ void k_block_stats(BlockStatArgs A);
 __global__ void k_find_peaks(PeakArgs A);

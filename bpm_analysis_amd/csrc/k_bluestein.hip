@@ -5,11 +5,11 @@
  * every recording the fused in-LDS kernel (k_hilbert.hip) cannot hold.
  *
  * An N-point DFT of arbitrary N (C5's ragged lengths have large prime
- * factors) becomes a cyclic convolution of length L = 2^k >= 2M - 1:
+ * factors) becomes a cyclic convolution of length L >= 2M - 1 (2^k or 3 * 2^k):
  *     X_k = c_k sum_n (x_n c_n) conj(c_(k-n)),   c_m = exp(-i pi m^2 / M),
  * computed as IFFT_L(FFT_L(x c) * FFT_L(b)) with b_m = conj(c_|m|) wrapped;
  * the inverse DFT uses conj(FFT_L(b)) (b is symmetric).  All recordings of
- * one (L, packing) group share two batched power-of-two rocFFT plans
+ * one (L, packing) group share two batched rocFFT plans
  * (forward, backward), so a ragged batch costs a handful of large batched
  * transforms instead of one small plan per distinct length.
  *
@@ -227,8 +227,11 @@ int bluestein_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb
         const int64_t N = doff[f + 1] - doff[f];
         const int pack = (N % 2) == 0;
         const int64_t M = pack ? N / 2 : N;
+        /* L = 2^k or 3 * 2^k (both fast rocFFT lengths): ~1.2x the needed
+         * 2M - 1 on average instead of ~1.4x, at most two groups per octave */
         int64_t L = 1;
         while (L < 2 * M - 1) L <<= 1;
+        if ((L >> 2) * 3 >= 2 * M - 1 && L >= 4) L = (L >> 2) * 3;
         groups[{pack, L}].push_back(f);
     }
     /* host copies outlive the async uploads; the FFT(b) tables depend on the

@@ -1,8 +1,8 @@
 /*
  * k_detect.hip — quantiles, block statistics and find_peaks.
  *
- *   k_quantile     np.quantile(env, q) 'linear' (bpm_analysis.py:1067, :225,
- *                  :1075, :1114): exact order statistics by 8-bit radix select
+ *   k_quantile_reg / k_ql_*  np.quantile(env, q) 'linear' (bpm_analysis.py:1067,
+ *                  :225, :1075, :1114): exact order statistics by radix select
  *                  on order-preserving f64 keys, then numpy's _lerp.
  *   k_block_stats  max/min of env per 64-sample block (prominence accelerator).
  *   k_find_peaks   scipy.signal.find_peaks(sign*env, height, distance,
@@ -29,81 +29,148 @@
 namespace bpmx {
 
 /* ------------------------------------------------------------------------ */
-constexpr int KQ_T = 1024;   /* long recordings: one workgroup per (recording, level), 16 waves */
-__global__ __launch_bounds__(KQ_T) void k_quantile(QuantArgs A) {
-    const int f = blockIdx.x, l = blockIdx.y;
-    if (f >= A.n_files || l >= A.n_levels || !A.active[f] || (A.skip && A.skip[f])) return;
-    const int64_t n = A.doff[f + 1] - A.doff[f];
-    if (n <= A.skip_le) return;
-    const double *x = A.env + A.doff[f];
-    const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-    __shared__ unsigned int hist[256];
-    __shared__ long long s_r;
-    __shared__ int s_digit;
-    __shared__ unsigned long long s_min[KQ_T / 64];
-    __shared__ long long s_cnt[KQ_T / 64];
+/* ------------------------------------------------------------------------ */
+/* the same quantiles for long recordings over many workgroups: k_ql_init sets
+ * each (recording, level)'s rank; per 11-bit digit (most significant first)
+ * k_ql_hist counts the keys that match the prefix found so far, every chunk
+ * of every recording in its own workgroup (LDS bins per level, merged into
+ * global bins), and k_ql_select picks the digit holding the rank; after six
+ * passes the prefix is the order statistic's key.  The next order statistic
+ * is the same key when the final bin holds another one, else the smallest key
+ * above it (k_ql_next), then numpy's _lerp (k_ql_final). */
+namespace {
+__device__ __forceinline__ bool ql_sel(const QuantArgs &Q, int f) {
+    if (f >= Q.n_files || !Q.active[f] || (Q.skip && Q.skip[f])) return false;
+    return Q.doff[f + 1] - Q.doff[f] > Q.skip_le;
+}
+__device__ __forceinline__ int ql_shift(int pass) {            /* 53, 42, 31, 20, 9, 0 (last digit 9 bits) */
+    return pass < QL_PASSES - 1 ? 64 - QL_BITS * (pass + 1) : 0;
+}
+}  // namespace
 
-    const double q = A.q[l];
-    const double vi = (double)(n - 1) * q;
-    const bool top = vi >= (double)(n - 1);
-    const long long lo = top ? (long long)(n - 1) : (long long)floor(vi);
-    uint64_t prefix = 0, mask = 0;
-    long long r = lo;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-        if (tid < 256) hist[tid] = 0;
-        __syncthreads();
-        for (int64_t i = tid; i < n; i += KQ_T) {
-            uint64_t k = f64_key(x[i]);
-            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
-        }
-        __syncthreads();
-        if (wid == 0) {
-            unsigned int c0 = hist[lane * 4], c1 = hist[lane * 4 + 1], c2 = hist[lane * 4 + 2], c3 = hist[lane * 4 + 3];
-            long long s = (long long)c0 + c1 + c2 + c3, incl = s;
-            for (int o = 1; o < 64; o <<= 1) {
-                long long t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            long long excl = incl - s;
-            if (excl <= r && r < incl) {
-                long long rr = r - excl;
-                unsigned int cs[4] = {c0, c1, c2, c3};
-                int d = 0;
-                while (rr >= (long long)cs[d]) { rr -= cs[d]; ++d; }
-                s_digit = lane * 4 + d;
-                s_r = rr;
-            }
-        }
-        __syncthreads();
-        prefix |= (uint64_t)s_digit << shift;
-        mask |= 0xFFull << shift;
-        r = s_r;
-        __syncthreads();
+__global__ __launch_bounds__(64) void k_ql_init(QlArgs A) {
+    const int f = blockIdx.x, l = threadIdx.x;
+    if (!ql_sel(A.Q, f) || l >= A.Q.n_levels) return;
+    const int64_t n = A.Q.doff[f + 1] - A.Q.doff[f];
+    const double vi = (double)(n - 1) * A.Q.q[l];
+    QlState s;
+    s.top = vi >= (double)(n - 1);
+    s.lo = s.top ? (long long)(n - 1) : (long long)floor(vi);
+    s.r = s.lo;
+    s.prefix = 0; s.mask = 0; s.next = ~0ull; s.eq = 0;
+    A.st[(int64_t)f * Q_SLOTS + l] = s;
+}
+
+__global__ __launch_bounds__(256) void k_ql_hist(QlArgs A) {
+    const int f = blockIdx.y;
+    if (!ql_sel(A.Q, f)) return;
+    const int64_t d0 = A.Q.doff[f], n = A.Q.doff[f + 1] - d0;
+    const int64_t c0 = (int64_t)blockIdx.x * QL_CHUNK;
+    if (c0 >= n) return;
+    const int64_t c1 = min<int64_t>(n, c0 + QL_CHUNK);
+    const int L = A.Q.n_levels, sh = ql_shift(A.pass);
+    const unsigned int dmask = A.pass < QL_PASSES - 1 ? (unsigned)(QL_BINS - 1) : 511u;
+    __shared__ unsigned int hist[Q_SLOTS][QL_BINS];
+    __shared__ unsigned long long s_pre[Q_SLOTS], s_msk[Q_SLOTS];
+    for (int i = threadIdx.x; i < L * QL_BINS; i += 256) hist[i / QL_BINS][i % QL_BINS] = 0u;
+    if (threadIdx.x < L) {
+        const QlState st = A.st[(int64_t)f * Q_SLOTS + threadIdx.x];
+        s_pre[threadIdx.x] = st.prefix;
+        s_msk[threadIdx.x] = st.mask;
     }
-    const double va = key_f64(prefix);
-    double res = va;
-    if (!top) {
-        unsigned long long mn = ~0ull;
-        long long cnt = 0;
-        for (int64_t i = tid; i < n; i += KQ_T) {
-            uint64_t k = f64_key(x[i]);
-            if (k <= prefix) cnt++;
-            else if (k < mn) mn = k;
-        }
+    __syncthreads();
+    const double *x = A.Q.env + d0;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+        const uint64_t k = f64_key(x[i]);
+        const unsigned int dg = (unsigned int)(k >> sh) & dmask;
+        for (int l = 0; l < L; ++l)
+            if ((k & s_msk[l]) == s_pre[l]) atomicAdd(&hist[l][dg], 1u);
+    }
+    __syncthreads();
+    unsigned int *g = A.hist + (((int64_t)A.pass * A.Q.n_files + f) * Q_SLOTS) * QL_BINS;
+    for (int i = threadIdx.x; i < L * QL_BINS; i += 256) {
+        const unsigned int c = hist[i / QL_BINS][i % QL_BINS];
+        if (c) atomicAdd(&g[(i / QL_BINS) * QL_BINS + (i % QL_BINS)], c);
+    }
+}
+
+/* one workgroup per (recording, level): the digit whose cumulative count passes r */
+__global__ __launch_bounds__(256) void k_ql_select(QlArgs A) {
+    const int f = blockIdx.x, l = blockIdx.y;
+    if (!ql_sel(A.Q, f) || l >= A.Q.n_levels) return;
+    const unsigned int *g = A.hist + (((int64_t)A.pass * A.Q.n_files + f) * Q_SLOTS + l) * QL_BINS;
+    QlState *ps = A.st + (int64_t)f * Q_SLOTS + l;
+    const long long r = ps->r;
+    __shared__ int sh[256 / 64 + 1];
+    constexpr int PER = QL_BINS / 256;                          /* 8 consecutive bins per thread */
+    unsigned int c[PER];
+    int sum = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) { c[u] = g[threadIdx.x * PER + u]; sum += (int)c[u]; }
+    int tot;
+    const long long before = block_scan_int<256>(sum, sh, &tot);
+    if (before <= r && r < before + sum) {                       /* exactly one thread */
+        long long rr = r - before;
+        int d = 0;
+        while (rr >= (long long)c[d]) { rr -= c[d]; ++d; }
+        const int digit = threadIdx.x * PER + d, s = ql_shift(A.pass);
+        const unsigned long long dm = A.pass < QL_PASSES - 1 ? (unsigned long long)(QL_BINS - 1) : 511ull;
+        ps->prefix |= (unsigned long long)digit << s;
+        ps->mask |= dm << s;
+        ps->r = rr;
+        if (A.pass == QL_PASSES - 1) ps->eq = (long long)c[d] > rr + 1 ? 1 : 0;   /* another key equals it */
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ql_next(QlArgs A) {
+    const int f = blockIdx.y;
+    if (!ql_sel(A.Q, f)) return;
+    const int64_t d0 = A.Q.doff[f], n = A.Q.doff[f + 1] - d0;
+    const int64_t c0 = (int64_t)blockIdx.x * QL_CHUNK;
+    if (c0 >= n) return;
+    const int64_t c1 = min<int64_t>(n, c0 + QL_CHUNK);
+    const int L = A.Q.n_levels;
+    __shared__ unsigned long long s_pre[Q_SLOTS];
+    __shared__ int s_need[Q_SLOTS];
+    if (threadIdx.x < L) {
+        const QlState st = A.st[(int64_t)f * Q_SLOTS + threadIdx.x];
+        s_pre[threadIdx.x] = st.prefix;
+        s_need[threadIdx.x] = !st.top && !st.eq;
+    }
+    __syncthreads();
+    unsigned long long mn[Q_SLOTS] = {~0ull, ~0ull, ~0ull, ~0ull};
+    const double *x = A.Q.env + d0;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+        const uint64_t k = f64_key(x[i]);
+#pragma unroll
+        for (int l = 0; l < Q_SLOTS; ++l)
+            if (l < L && k > s_pre[l] && k < mn[l]) mn[l] = k;
+    }
+#pragma unroll
+    for (int l = 0; l < Q_SLOTS; ++l) {
+        if (l >= L || !s_need[l]) continue;
+        unsigned long long m = mn[l];
         for (int o = 32; o > 0; o >>= 1) {
-            unsigned long long om = __shfl_xor(mn, o);
-            mn = om < mn ? om : mn;
-            cnt += __shfl_xor(cnt, o);
+            const unsigned long long om = __shfl_xor(m, o);
+            m = om < m ? om : m;
         }
-        if (lane == 0) { s_min[wid] = mn; s_cnt[wid] = cnt; }
-        __syncthreads();
-        unsigned long long m = s_min[0];
-        long long c = 0;
-        for (int w = 0; w < KQ_T / 64; ++w) { m = s_min[w] < m ? s_min[w] : m; c += s_cnt[w]; }
-        const double vb = (c > lo + 1) ? va : key_f64(m);
-        res = np_lerp(va, vb, vi - (double)lo);
+        if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(&A.st[(int64_t)f * Q_SLOTS + l].next, m);
     }
-    if (tid < Q_SLOTS && ((A.slot[l] >> tid) & 1)) A.qv[(int64_t)f * Q_SLOTS + tid] = res;
+}
+
+__global__ __launch_bounds__(64) void k_ql_final(QlArgs A) {
+    const int f = blockIdx.x, l = threadIdx.x;
+    if (!ql_sel(A.Q, f) || l >= A.Q.n_levels) return;
+    const int64_t n = A.Q.doff[f + 1] - A.Q.doff[f];
+    const QlState st = A.st[(int64_t)f * Q_SLOTS + l];
+    const double va = key_f64(st.prefix);
+    double res = va;
+    if (!st.top) {
+        const double vb = st.eq ? va : key_f64(st.next);
+        res = np_lerp(va, vb, (double)(n - 1) * A.Q.q[l] - (double)st.lo);
+    }
+    for (int s = 0; s < Q_SLOTS; ++s)
+        if ((A.Q.slot[l] >> s) & 1) A.Q.qv[(int64_t)f * Q_SLOTS + s] = res;
 }
 
 /* ------------------------------------------------------------------------ */
