@@ -706,7 +706,11 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     __shared__ double s_mh[FL_MC];
     __shared__ double s_vv[FL_MC + 1];
     __shared__ uint8_t s_st[FL_MC];
-    __shared__ double s_bh[FL_MC / 32], s_bvl[FL_MC / 32], s_bvr[FL_MC / 32];
+    /* block summaries for the prominence walks at 8, 64 and 512 maxima:
+     * max height, min of the gap valleys a left walk crosses (vv[k + 1]) and
+     * a right walk crosses (vv[k]) */
+    constexpr int FL_B1 = FL_MC / 8, FL_B2 = FL_MC / 64, FL_B3 = FL_MC / 512;
+    __shared__ double s_bh[FL_B1 + FL_B2 + FL_B3], s_bvl[FL_B1 + FL_B2 + FL_B3], s_bvr[FL_B1 + FL_B2 + FL_B3];
     __shared__ int s_gc[2][FP_G][NW];
     __shared__ int sh[NW + 1];
     __shared__ int s_flag;
@@ -793,30 +797,72 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     __syncthreads();
     STAMP(2);
 
-    /* (3) distance: rounds of local decisions (k_find_peaks' rule) */
+    /* (3) distance: rounds of local decisions (k_find_peaks' rule: a
+     * candidate is removed once a higher-priority candidate within `dist` is
+     * kept, kept once none is undecided).  Positions and heights do not
+     * change, so each candidate's higher-priority neighbours (left: strictly
+     * higher, right: at least as high) are listed once, up to four in
+     * registers; a round then only reads their states. */
+#ifdef BPMX_FP_NODIST
+    if (false) {
+#else
     if (dist > 1) {
+#endif
+        constexpr int FP_R = FL_MC / FP_T;
+        uint32_t nb[FP_R][2];                                /* four 16-bit neighbour indices */
+        int nbc[FP_R];                                       /* count; -1: more than four (full scan) */
+#pragma unroll
+        for (int r = 0; r < FP_R; ++r) {
+            const int j = tid + r * FP_T;
+            nb[r][0] = nb[r][1] = 0u;
+            nbc[r] = 0;
+            if (j >= M || s_st[j] != ST_UNDECIDED) continue;
+            const int64_t pj = s_mp[j];
+            const double vj = s_mh[j];
+            int c = 0;
+            auto add = [&](int k) {
+                if (c < 4) nb[r][c >> 1] |= (uint32_t)k << (16 * (c & 1));
+                ++c;
+            };
+            for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k)
+                if (s_mh[k] > vj && s_st[k] == ST_UNDECIDED) add(k);
+            for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k)
+                if (s_mh[k] >= vj && s_st[k] == ST_UNDECIDED) add(k);
+            nbc[r] = c <= 4 ? c : -1;
+        }
         for (int round = 0; round <= M; ++round) {
             if (tid == 0) s_flag = 0;
             __syncthreads();
             bool pending = false;
-            for (int j = tid; j < M; j += FP_T) {
-                if (ld_state(&s_st[j]) != ST_UNDECIDED) continue;
-                const int64_t pj = s_mp[j];
-                const double vj = s_mh[j];
+#pragma unroll
+            for (int r = 0; r < FP_R; ++r) {
+                const int j = tid + r * FP_T;
+                if (j >= M || ld_state(&s_st[j]) != ST_UNDECIDED) continue;
                 bool killed = false, blocked = false;
-                for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
-                    if (s_mh[k] > vj) {
+                if (nbc[r] >= 0) {
+                    for (int q = 0; q < nbc[r]; ++q) {
+                        const int k = (int)((nb[r][q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
                         const uint8_t st = ld_state(&s_st[k]);
-                        if (st == ST_KEPT) { killed = true; break; }
-                        if (st == ST_UNDECIDED) blocked = true;
+                        killed |= st == ST_KEPT;
+                        blocked |= st == ST_UNDECIDED;
                     }
-                }
-                if (!killed) {
-                    for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k) {
-                        if (s_mh[k] >= vj) {
+                } else {
+                    const int64_t pj = s_mp[j];
+                    const double vj = s_mh[j];
+                    for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
+                        if (s_mh[k] > vj) {
                             const uint8_t st = ld_state(&s_st[k]);
                             if (st == ST_KEPT) { killed = true; break; }
                             if (st == ST_UNDECIDED) blocked = true;
+                        }
+                    }
+                    if (!killed) {
+                        for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k) {
+                            if (s_mh[k] >= vj) {
+                                const uint8_t st = ld_state(&s_st[k]);
+                                if (st == ST_KEPT) { killed = true; break; }
+                                if (st == ST_UNDECIDED) blocked = true;
+                            }
                         }
                     }
                 }
@@ -835,37 +881,57 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
 
     /* (4) prominences of the kept maxima, one thread each: walk the maxima
      * outwards to the nearest higher one, taking the gap valleys passed on the
-     * way; runs of 32 maxima that are all no higher are skipped whole through
-     * their block maximum and block valley minimum */
+     * way; aligned runs of 512, 64 or 8 maxima that are all no higher are
+     * skipped whole through their block maximum and block valley minimum */
     {
-        const int NB32 = (M + 31) >> 5;
-        for (int b = tid; b < NB32; b += FP_T) {
+        /* level 1 (8 maxima) from the maxima, levels 2 and 3 from the level below */
+        const int N1 = (M + 7) >> 3, N2 = (M + 63) >> 6, N3 = (M + 511) >> 9;
+        for (int b = tid; b < N1; b += FP_T) {
             double hx = -INF, vl = INF, vr = INF;
-            for (int k = b * 32; k < min(M, b * 32 + 32); ++k) {
+            for (int k = b * 8; k < min(M, b * 8 + 8); ++k) {
                 hx = fmax(hx, s_mh[k]);
-                vl = fmin(vl, s_vv[k + 1]);                  /* gaps k (left walks)       */
-                vr = fmin(vr, s_vv[k]);                      /* gaps k - 1 (right walks) */
+                vl = fmin(vl, s_vv[k + 1]);
+                vr = fmin(vr, s_vv[k]);
             }
-            s_bh[b] = hx;
-            s_bvl[b] = vl;
-            s_bvr[b] = vr;
+            s_bh[b] = hx; s_bvl[b] = vl; s_bvr[b] = vr;
         }
         __syncthreads();
+        for (int lv = 0; lv < 2; ++lv) {
+            const int src = lv == 0 ? 0 : FL_B1, dst = lv == 0 ? FL_B1 : FL_B1 + FL_B2;
+            const int nd_ = lv == 0 ? N2 : N3, ns_ = lv == 0 ? N1 : N2;
+            for (int b = tid; b < nd_; b += FP_T) {
+                double hx = -INF, vl = INF, vr = INF;
+                for (int c = b * 8; c < min(ns_, b * 8 + 8); ++c) {
+                    hx = fmax(hx, s_bh[src + c]);
+                    vl = fmin(vl, s_bvl[src + c]);
+                    vr = fmin(vr, s_bvr[src + c]);
+                }
+                s_bh[dst + b] = hx; s_bvl[dst + b] = vl; s_bvr[dst + b] = vr;
+            }
+            __syncthreads();
+        }
         const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
+        const double *bh2 = s_bh + FL_B1, *bh3 = s_bh + FL_B1 + FL_B2;
         for (int j = tid; j < M; j += FP_T) {
             if (s_st[j] != ST_KEPT) continue;
             const double hj = s_mh[j];
             double lmin = INF, rmin = INF;
+            /* left: at k, the largest aligned block ending at k with no higher maximum */
             for (int k = j - 1;;) {
                 if (k < 0) { lmin = fmin(lmin, s_vv[0]); break; }
-                if ((k & 31) == 31 && s_bh[k >> 5] <= hj) { lmin = fmin(lmin, s_bvl[k >> 5]); k -= 32; continue; }
+                if ((k & 511) == 511 && bh3[k >> 9] <= hj) { lmin = fmin(lmin, s_bvl[FL_B1 + FL_B2 + (k >> 9)]); k -= 512; continue; }
+                if ((k & 63) == 63 && bh2[k >> 6] <= hj) { lmin = fmin(lmin, s_bvl[FL_B1 + (k >> 6)]); k -= 64; continue; }
+                if ((k & 7) == 7 && s_bh[k >> 3] <= hj) { lmin = fmin(lmin, s_bvl[k >> 3]); k -= 8; continue; }
                 lmin = fmin(lmin, s_vv[k + 1]);
                 if (s_mh[k] > hj) break;
                 --k;
             }
+            /* right: the largest aligned full block starting at k with no higher maximum */
             for (int k = j + 1;;) {
                 if (k >= M) { rmin = fmin(rmin, s_vv[M]); break; }
-                if ((k & 31) == 0 && k + 31 < M && s_bh[k >> 5] <= hj) { rmin = fmin(rmin, s_bvr[k >> 5]); k += 32; continue; }
+                if ((k & 511) == 0 && k + 511 < M && bh3[k >> 9] <= hj) { rmin = fmin(rmin, s_bvr[FL_B1 + FL_B2 + (k >> 9)]); k += 512; continue; }
+                if ((k & 63) == 0 && k + 63 < M && bh2[k >> 6] <= hj) { rmin = fmin(rmin, s_bvr[FL_B1 + (k >> 6)]); k += 64; continue; }
+                if ((k & 7) == 0 && k + 7 < M && s_bh[k >> 3] <= hj) { rmin = fmin(rmin, s_bvr[k >> 3]); k += 8; continue; }
                 rmin = fmin(rmin, s_vv[k]);
                 if (s_mh[k] > hj) break;
                 ++k;
