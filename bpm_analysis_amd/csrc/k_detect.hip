@@ -713,7 +713,6 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     __shared__ double s_bh[FL_B1 + FL_B2 + FL_B3], s_bvl[FL_B1 + FL_B2 + FL_B3], s_bvr[FL_B1 + FL_B2 + FL_B3];
     __shared__ int s_gc[2][FP_G][NW];
     __shared__ int sh[NW + 1];
-    __shared__ int s_flag;
     STAMP_DECL
 
     /* (1) local maxima (plateau midpoints) and valley starts, in order: wave w
@@ -830,51 +829,56 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
                 if (s_mh[k] >= vj && s_st[k] == ST_UNDECIDED) add(k);
             nbc[r] = c <= 4 ? c : -1;
         }
-        for (int round = 0; round <= M; ++round) {
-            if (tid == 0) s_flag = 0;
-            __syncthreads();
+        STAMP(6);
+        /* Rounds run wave-locally (a candidate's neighbours are mostly in its
+         * own wave: lanes j +- 1 ...) until the wave makes no progress; one
+         * workgroup barrier then lets decisions cross wave boundaries.  A
+         * decision needs a KEPT neighbour (final) or no UNDECIDED one (a stale
+         * read only delays it), so unsynchronised reads are safe. */
+        for (int gi = 0; gi <= M; ++gi) {
             bool pending = false;
+            for (int lr = 0; lr <= M; ++lr) {
+                bool progress = false;
+                pending = false;
 #pragma unroll
-            for (int r = 0; r < FP_R; ++r) {
-                const int j = tid + r * FP_T;
-                if (j >= M || ld_state(&s_st[j]) != ST_UNDECIDED) continue;
-                bool killed = false, blocked = false;
-                if (nbc[r] >= 0) {
-                    for (int q = 0; q < nbc[r]; ++q) {
-                        const int k = (int)((nb[r][q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
-                        const uint8_t st = ld_state(&s_st[k]);
-                        killed |= st == ST_KEPT;
-                        blocked |= st == ST_UNDECIDED;
-                    }
-                } else {
-                    const int64_t pj = s_mp[j];
-                    const double vj = s_mh[j];
-                    for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
-                        if (s_mh[k] > vj) {
+                for (int r = 0; r < FP_R; ++r) {
+                    const int j = tid + r * FP_T;
+                    if (j >= M || ld_state(&s_st[j]) != ST_UNDECIDED) continue;
+                    bool killed = false, blocked = false;
+                    if (nbc[r] >= 0) {
+                        for (int q = 0; q < nbc[r]; ++q) {
+                            const int k = (int)((nb[r][q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
                             const uint8_t st = ld_state(&s_st[k]);
-                            if (st == ST_KEPT) { killed = true; break; }
-                            if (st == ST_UNDECIDED) blocked = true;
+                            killed |= st == ST_KEPT;
+                            blocked |= st == ST_UNDECIDED;
                         }
-                    }
-                    if (!killed) {
-                        for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k) {
-                            if (s_mh[k] >= vj) {
+                    } else {
+                        const int64_t pj = s_mp[j];
+                        const double vj = s_mh[j];
+                        for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
+                            if (s_mh[k] > vj) {
                                 const uint8_t st = ld_state(&s_st[k]);
                                 if (st == ST_KEPT) { killed = true; break; }
                                 if (st == ST_UNDECIDED) blocked = true;
                             }
                         }
+                        if (!killed) {
+                            for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k) {
+                                if (s_mh[k] >= vj) {
+                                    const uint8_t st = ld_state(&s_st[k]);
+                                    if (st == ST_KEPT) { killed = true; break; }
+                                    if (st == ST_UNDECIDED) blocked = true;
+                                }
+                            }
+                        }
                     }
+                    if (killed) { st_state(&s_st[j], ST_REMOVED); progress = true; }
+                    else if (!blocked) { st_state(&s_st[j], ST_KEPT); progress = true; }
+                    else pending = true;
                 }
-                if (killed) st_state(&s_st[j], ST_REMOVED);
-                else if (!blocked) st_state(&s_st[j], ST_KEPT);
-                else pending = true;
+                if (!__ballot(progress)) break;                  /* wave-uniform */
             }
-            if (pending) s_flag = 1;
-            __syncthreads();
-            const int again = s_flag;
-            __syncthreads();
-            if (!again) break;
+            if (!__syncthreads_or(pending)) break;
         }
     }
     STAMP(3);

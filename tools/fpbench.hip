@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
         long long np = 0;
         for (auto v : no) np += v;
         const char *names0[8] = {"tables", "maxima", "distance", "prominence", "compact", "(prom max wave)", "(prom mean wave)", "-"};
-        const char *names1[8] = {"-", "extrema", "to LDS", "distance", "prominence", "compact", "-", "-"};
+        const char *names1[8] = {"-", "extrema", "to LDS", "dist:rounds", "prominence", "compact", "dist:lists", "-"};
         const char **names = lds ? names1 : names0;
         printf("sign %+.0f: %.3f ms, %lld peaks; per-WG cycles %.0f\n", sg, best, np, tot / F);
         for (int k = 0; k < 8; ++k)
