@@ -22,11 +22,25 @@ constexpr size_t HB_LDS_MAX = 160 * 1024;  /* one workgroup per CU */
 constexpr int HB_MF_PMIN = 31;             /* odd-prime stages from here on run on the matrix cores (23: slower) */
 constexpr int HB_MF_UNITS = 2;             /* 16 x 16 output tiles per wave in such a stage */
 
+/* x / d for 0 <= x, x d < 2^32 by one 32x64-bit multiply: m = floor((2^32 - 1) / d) + 1
+ * exceeds 2^32 / d by at most 1, so x m / 2^32 = x / d + eps with eps < 1 / d
+ * (exact floor).  The plan's divisors times the kernel's dividends stay
+ * below 2^32 (hilbert_plan checks M). */
+__host__ __device__ inline uint64_t hb_magic(uint32_t d) { return 0xFFFFFFFFull / d + 1ull; }
+__device__ __forceinline__ int hb_div(int x, uint64_t m) { return (int)(((uint64_t)(uint32_t)x * m) >> 32); }
+
 struct HilbPlan {
     int32_t M, N, ns, ntwh, nptab, window;
     int32_t rad[HB_MAXS], B[HB_MAXS], L[HB_MAXS], ptab[HB_MAXS];
     int32_t mf[HB_MAXS];           /* stage runs as an f64 MFMA GEMM (hb_radixp_mfma) */
+    /* magic multipliers (hb_magic) of the stage's divisors: L, radix p,
+     * h = (p - 1) / 2, k groups (h + HB_KB) / HB_KB, MFMA column tiles (h + 16) / 16 */
+    uint64_t dL[HB_MAXS], dP[HB_MAXS], dH[HB_MAXS], dG[HB_MAXS], dT[HB_MAXS];
+    int32_t rd[HB_MAXS];           /* stage runs as Rader's 197-point DFT (hb_rader197) */
+    int32_t nrtab;                 /* Rader tables after the prime tables: FFT_196(b) / 196 | W_196^e */
+    int32_t per;                   /* rolling-mean outputs per thread, ceil(N / HB_T) */
 };
+constexpr int HB_RD_P = 197;               /* Rader: 197 - 1 = 14 x 14, the 14-point DFTs as 2 x 7 prime-factor */
 
 struct HilbArgs {
     const double *yd;              /* [sumNd] decimated filtered signal */
@@ -42,7 +56,7 @@ __global__ void k_hilbert_env(HilbArgs A, HilbPlan P);
 
 /* 1 and the plan, its tables and LDS size when Nd takes the fused kernel; 0 otherwise */
 int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes,
-                 bool mfma = true);
+                 bool mfma = true, bool rader = true);
 
 }  // namespace bpmx
 

@@ -47,10 +47,12 @@ struct HbLds {
 
 /* radix-2 stage: DIF (twiddle after) or DIT inverse (conjugate twiddle before) */
 template <bool INV>
-__device__ __forceinline__ void hb_radix2(const HbLds &S, int M, int N, int B, int L) {
-    const int nb = M / 2, step = N / B;
+__device__ __forceinline__ void hb_radix2(const HbLds &S, const HilbPlan &P, int si) {
+    const int M = P.M, B = P.B[si], L = P.L[si];
+    const uint64_t dL = P.dL[si];
+    const int nb = M / 2, step = P.N / B;
     for (int t = threadIdx.x; t < nb; t += HB_T) {
-        const int blk = t / L, n2 = t - blk * L, base = blk * B + n2;
+        const int blk = hb_div(t, dL), n2 = t - blk * L, base = blk * B + n2;
         double2 a = S.x[base], b = S.x[base + L];
         if (!INV) {
             const double2 d = csub(a, b);
@@ -67,12 +69,14 @@ __device__ __forceinline__ void hb_radix2(const HbLds &S, int M, int N, int B, i
 
 /* odd prime radix p, pair-symmetric direct DFT */
 template <bool INV>
-__device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, int L, int p, const double2 *ct) {
-    const int h = (p - 1) >> 1, nbf = M / p, step = N / B;
+__device__ __forceinline__ void hb_radixp(const HbLds &S, const HilbPlan &P, int si, const double2 *ct) {
+    const int M = P.M, B = P.B[si], L = P.L[si], p = P.rad[si];
+    const uint64_t dL = P.dL[si], dP = P.dP[si], dH = P.dH[si], dG = P.dG[si];
+    const int h = (p - 1) >> 1, nbf = M / p, step = P.N / B;
     /* pre-pass: (DIT: conjugate twiddles, then) x_n, x_(p-n) -> a_n = x_n + x_(p-n), b_n = x_n - x_(p-n) */
     for (int t = threadIdx.x; t < nbf * h; t += HB_T) {
-        const int bf = t / h, n = t - bf * h + 1;
-        const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+        const int bf = hb_div(t, dH), n = t - bf * h + 1;
+        const int blk = hb_div(bf, dL), n2 = bf - blk * L, base = blk * B + n2;
         double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
         if (INV && n2) {
             u = cmulc(u, S.tw(step * n2 * n));
@@ -95,8 +99,8 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
     for (int i = 0; i < HB_MAXT; ++i) {
         const int t = threadIdx.x + i * HB_T;
         if (t < ntask) {
-            const int bf = t / ng, k0 = (t - bf * ng) * HB_KB;
-            const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+            const int bf = hb_div(t, dG), k0 = (t - bf * ng) * HB_KB;
+            const int blk = hb_div(bf, dL), n2 = bf - blk * L, base = blk * B + n2;
             const double2 x0 = S.x[base];
             double ax[HB_KB], ay[HB_KB], bx[HB_KB], by[HB_KB], c[HB_KB], cp[HB_KB], sn[HB_KB], sp[HB_KB], c2[HB_KB];
             int idx[HB_KB];
@@ -118,7 +122,7 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
                     const double2 e0 = ct[idx[j]], e1 = ct[i1];
                     cp[j] = e0.x; sp[j] = e0.y; c[j] = e1.x; sn[j] = e1.y;
                     int i16 = i1 + 15 * k;                         /* ((n0 + 15) k) mod p */
-                    i16 -= (i16 / p) * p;
+                    i16 -= hb_div(i16, dP) * p;
                     idx[j] = i16;
                 }
                 const int n1 = n0 + 16 <= h + 1 ? n0 + 16 : h + 1;
@@ -164,8 +168,8 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
     for (int i = 0; i < HB_MAXT; ++i) {
         const int t = threadIdx.x + i * HB_T;
         if (t < ntask) {
-            const int bf = t / ng, k0 = (t - bf * ng) * HB_KB;
-            const int blk = bf / L, n2 = bf - blk * L, base = blk * B + n2;
+            const int bf = hb_div(t, dG), k0 = (t - bf * ng) * HB_KB;
+            const int blk = hb_div(bf, dL), n2 = bf - blk * L, base = blk * B + n2;
 #pragma unroll
             for (int j = 0; j < HB_KB; ++j) {
                 const int k = k0 + j;
@@ -197,12 +201,14 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, int M, int N, int B, i
  * read, then the DIF twiddles are applied on the way out. */
 typedef double hb_d4 __attribute__((ext_vector_type(4)));
 template <bool INV, bool CONTIG>
-__device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int B, int Lr, int p, const double2 *ct) {
-    const int L = CONTIG ? 1 : Lr;                             /* contiguous stage: no index divisions */
-    const int h = (p - 1) >> 1, nbf = M / p, step = N / B;
+__device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, const HilbPlan &P, int si, const double2 *ct) {
+    const int M = P.M, B = P.B[si], p = P.rad[si];
+    const int L = CONTIG ? 1 : P.L[si];                        /* contiguous stage: no index divisions */
+    const uint64_t dL = P.dL[si], dP = P.dP[si], dH = P.dH[si], dT = P.dT[si];
+    const int h = (p - 1) >> 1, nbf = M / p, step = P.N / B;
     for (int t = threadIdx.x; t < nbf * h; t += HB_T) {
-        const int bf = t / h, n = t - bf * h + 1;
-        const int blk = CONTIG ? bf : bf / L, n2 = CONTIG ? 0 : bf - blk * L, base = CONTIG ? bf * p : blk * B + n2;
+        const int bf = hb_div(t, dH), n = t - bf * h + 1;
+        const int blk = CONTIG ? bf : hb_div(bf, dL), n2 = CONTIG ? 0 : bf - blk * L, base = CONTIG ? bf * p : blk * B + n2;
         double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
         if (INV && n2) {
             u = cmulc(u, S.tw(step * n2 * n));
@@ -216,7 +222,7 @@ __device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
     auto base_of = [&](int bf) {
         if (CONTIG) return bf * p;
-        const int blk = bf / L;
+        const int blk = hb_div(bf, dL);
         return blk * B + (bf - blk * L);
     };
     hb_d4 acc[HB_MF_UNITS][4];
@@ -225,13 +231,14 @@ __device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int
     for (int u = 0; u < HB_MF_UNITS; ++u) {
         const int unit = wv + u * (HB_T / 64);
         if (unit < units) {                                    /* wave-uniform */
-            const int m = unit / ntl, nt = unit - m * ntl;
+            const int m = hb_div(unit, dT), nt = unit - m * ntl;
             const int dA = 16 * m + r16, kB = 16 * nt + r16;
             const bool rowok = dA < nbf;
             const double2 *xa = S.x + base_of(rowok ? dA : 0);
             hb_d4 c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0, c2 = c0, c3 = c0;
-            int idx = ((kq + 1) * kB) % p;                     /* (n k) mod p, n = 4 s + kq + 1 */
-            const int st4 = (4 * kB) % p;
+            int idx = (kq + 1) * kB;                           /* (n k) mod p, n = 4 s + kq + 1 */
+            idx -= hb_div(idx, dP) * p;
+            const int st4 = 4 * kB - hb_div(4 * kB, dP) * p;
             for (int s = 0; s < ks; ++s) {
                 const int n = 4 * s + kq + 1;
                 const bool ok = rowok && n <= h;
@@ -258,12 +265,12 @@ __device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int
     for (int u = 0; u < HB_MF_UNITS; ++u) {
         const int unit = wv + u * (HB_T / 64);
         if (unit < units) {
-            const int m = unit / ntl, nt = unit - m * ntl, k = 16 * nt + r16;
+            const int m = hb_div(unit, dT), nt = unit - m * ntl, k = 16 * nt + r16;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int d = 16 * m + kq + 4 * r;
                 if (d < nbf && k <= h) {
-                    const int blk = CONTIG ? d : d / L, n2 = CONTIG ? 0 : d - blk * L, base = CONTIG ? d * p : blk * B + n2;
+                    const int blk = CONTIG ? d : hb_div(d, dL), n2 = CONTIG ? 0 : d - blk * L, base = CONTIG ? d * p : blk * B + n2;
                     const double are = acc[u][0][r], aim = acc[u][1][r], bre = acc[u][2][r], bim = acc[u][3][r];
                     const double2 xa = make_double2(x0[u][r].x + are, x0[u][r].y + aim);
                     /* forward: X_k = x0 + A - iB, X_(p-k) = x0 + A + iB; inverse: signs swapped */
@@ -283,10 +290,140 @@ __device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, int M, int N, int
     __syncthreads();
 }
 
+/* 7-point DFT in registers, pair-symmetric (forward e^(-2 pi i nk/7); INV: e^(+...)) */
+template <bool INV>
+__device__ __forceinline__ void hb_dft7(double2 (&x)[7]) {
+    constexpr double c1 = 0.6234898018587335, c2 = -0.2225209339563144, c3 = -0.9009688679024191;
+    constexpr double s1 = 0.7818314824680298, s2 = 0.9749279121818236, s3 = 0.4338837391175581;
+    const double2 a1 = cadd(x[1], x[6]), a2 = cadd(x[2], x[5]), a3 = cadd(x[3], x[4]);
+    const double2 b1 = csub(x[1], x[6]), b2 = csub(x[2], x[5]), b3 = csub(x[3], x[4]);
+    const double2 x0 = x[0];
+    auto A = [&](double ca, double cb, double cc) {
+        return make_double2(__builtin_fma(cc, a3.x, __builtin_fma(cb, a2.x, __builtin_fma(ca, a1.x, x0.x))),
+                            __builtin_fma(cc, a3.y, __builtin_fma(cb, a2.y, __builtin_fma(ca, a1.y, x0.y))));
+    };
+    auto Bs = [&](double sa, double sb, double sc) {
+        return make_double2(__builtin_fma(sc, b3.x, __builtin_fma(sb, b2.x, sa * b1.x)),
+                            __builtin_fma(sc, b3.y, __builtin_fma(sb, b2.y, sa * b1.y)));
+    };
+    /* cos / sin (2 pi n k / 7) for n = 1, 2, 3 at k = 1, 2, 3 */
+    const double2 A1 = A(c1, c2, c3), A2 = A(c2, c3, c1), A3 = A(c3, c1, c2);
+    const double2 B1 = Bs(s1, s2, s3), B2 = Bs(s2, -s3, -s1), B3 = Bs(s3, -s1, s2);
+    x[0] = make_double2(x0.x + a1.x + a2.x + a3.x, x0.y + a1.y + a2.y + a3.y);
+    auto put = [&](int k, double2 Ak, double2 Bk) {
+        /* forward: X_k = A - iB, X_(7-k) = A + iB; inverse: the other way */
+        const double2 mi = make_double2(Ak.x + Bk.y, Ak.y - Bk.x), pl = make_double2(Ak.x - Bk.y, Ak.y + Bk.x);
+        x[k] = INV ? pl : mi;
+        x[7 - k] = INV ? mi : pl;
+    };
+    put(1, A1, B1);
+    put(2, A2, B2);
+    put(3, A3, B3);
+}
+
+/* 14-point DFT in registers as the 2 x 7 prime-factor (Good-Thomas) split:
+ * input n = (7 n1 + 2 n2) mod 14, output k = (7 k1 + 8 k2) mod 14, no twiddles */
+template <bool INV>
+__device__ __forceinline__ void hb_dft14(double2 (&v)[14]) {
+    double2 u0[7], u1[7];
+#pragma unroll
+    for (int n2 = 0; n2 < 7; ++n2) {
+        const double2 a = v[(2 * n2) % 14], b = v[(7 + 2 * n2) % 14];
+        u0[n2] = cadd(a, b);
+        u1[n2] = csub(a, b);
+    }
+    hb_dft7<INV>(u0);
+    hb_dft7<INV>(u1);
+#pragma unroll
+    for (int k2 = 0; k2 < 7; ++k2) {
+        v[(8 * k2) % 14] = u0[k2];
+        v[(7 + 8 * k2) % 14] = u1[k2];
+    }
+}
+
+/* Rader's algorithm for the contiguous (L = 1, twiddle-free) radix-197 stage.
+ * With g = 2 a generator mod 197 and w = e^(-2 pi i / 197),
+ *   X_0 = sum_n x_n,  X_(g^-m) = x_0 + sum_q a_q b_(m-q)   (a_q = x_(g^q), b_j = w^(g^-j)),
+ * a 196-point cyclic convolution: IDFT_196(DFT_196(a) . DFT_196(b) / 196), the
+ * last factor a host table.  Each 196-point DFT is 14 x 14: thread (butterfly,
+ * column c) holds 14 points in registers, a 14-point DFT, the W_196 twiddles,
+ * one LDS exchange (row c), a 14-point DFT; the pointwise product and the
+ * inverse's first 14-point DFT follow in the same registers, then the second
+ * exchange and the last 14-point DFT.  The inverse stage (DIT, first in the
+ * inverse pass, also twiddle-free) is conj(DFT(conj x)).  About a quarter of
+ * the f64 operations of the pair-symmetric direct DFT. */
+template <bool INV>
+__device__ __forceinline__ void hb_rader197(const HbLds &S, const HilbPlan &P, const double2 *rt) {
+    constexpr int R = 14, PR = HB_RD_P;
+    const double2 *Bh = rt, *W = rt + (PR - 1);
+    const int nbf = P.M / PR, ntask = nbf * R;
+    auto cj = [](double2 z) { return INV ? make_double2(z.x, -z.y) : z; };
+    for (int t0 = 0; t0 < ntask; t0 += HB_T) {               /* uniform trip count: barriers inside */
+        const int t = t0 + (int)threadIdx.x;
+        const bool act = t < ntask;
+        const int f = act ? t / R : 0, c = act ? t - f * R : 0;
+        double2 *blk = S.x + f * PR;
+        double2 v[R], x0 = make_double2(0.0, 0.0), X0 = x0;
+        int gc = 1, gic = 1;                                 /* 2^c, 99^c = 2^-c mod 197 */
+        for (int j = 0; j < c; ++j) { gc = (gc * 2) % PR; gic = (gic * 99) % PR; }
+        if (act) {
+            x0 = cj(blk[0]);
+            int e = gc;                                      /* a_(14 n1 + c) = x_(2^c 33^n1) */
+#pragma unroll
+            for (int n1 = 0; n1 < R; ++n1) {
+                v[n1] = cj(blk[e]);
+                e = (e * 33) % PR;
+            }
+            hb_dft14<false>(v);
+#pragma unroll
+            for (int k1 = 1; k1 < R; ++k1) v[k1] = cmul(v[k1], W[c * k1]);
+        }
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int k1 = 0; k1 < R; ++k1) blk[1 + k1 * R + c] = v[k1];
+        }
+        __syncthreads();
+        if (act) {                                           /* this thread is row k1 = c */
+#pragma unroll
+            for (int n2 = 0; n2 < R; ++n2) v[n2] = blk[1 + c * R + n2];
+            hb_dft14<false>(v);                              /* v[k2] = DFT(a)[c + 14 k2] */
+            X0 = cadd(x0, v[0]);                             /* used by c == 0 only */
+#pragma unroll
+            for (int k2 = 0; k2 < R; ++k2) v[k2] = cmul(v[k2], Bh[c + R * k2]);
+            hb_dft14<true>(v);                               /* over k2 -> m2 */
+#pragma unroll
+            for (int m2 = 1; m2 < R; ++m2) v[m2] = cmulc(v[m2], W[c * m2]);
+        }
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int m2 = 0; m2 < R; ++m2) blk[1 + m2 * R + c] = v[m2];
+        }
+        __syncthreads();
+        if (act) {                                           /* this thread is column m2 = c */
+#pragma unroll
+            for (int k1 = 0; k1 < R; ++k1) v[k1] = blk[1 + c * R + k1];
+            hb_dft14<true>(v);                               /* v[m1] = conv[c + 14 m1] */
+        }
+        __syncthreads();
+        if (act) {
+            int e = gic;                                     /* X_(2^-(c + 14 m1)) = x_0 + conv */
+#pragma unroll
+            for (int m1 = 0; m1 < R; ++m1) {
+                blk[e] = cj(cadd(x0, v[m1]));
+                e = (e * 6) % PR;                            /* 99^14 = 6 mod 197 */
+            }
+            if (c == 0) blk[0] = cj(X0);
+        }
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ int hb_pos(const HilbPlan &P, int k) {     /* position of frequency k after the DIF */
     int pos = 0;
     for (int i = 0; i < P.ns; ++i) {
-        const int r = P.rad[i], q = k / r;
+        const int r = P.rad[i], q = hb_div(k, P.dP[i]);
         pos += (k - q * r) * P.L[i];
         k = q;
     }
@@ -305,16 +442,30 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     S.pt = S.twl + 128;
     const int64_t d0 = A.doff[f];
     const double2 *y2 = (const double2 *)(A.yd + d0);              /* doff is even: 16-B aligned (host checks) */
-    for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab; i += HB_T) S.twh[i] = A.tabs[i];
-    for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2[m];
+    /* a leading radix-2 stage over the whole transform (B = M) is fused into
+     * the load, a trailing one of the inverse into the magnitude */
+    const bool r2 = P.rad[0] == 2 && P.B[0] == M;
+    const int H = M / 2;
+    for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab + P.nrtab; i += HB_T) S.twh[i] = A.tabs[i];
+    if (!r2)
+        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2[m];
     __syncthreads();
     STAMP_DECL
+    if (r2) {
+        for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIF radix 2: L = M / 2, twiddle W_N^(2t) */
+            const double2 a = y2[t], b = y2[t + H], d = csub(a, b);
+            S.x[t] = cadd(a, b);
+            S.x[t + H] = t ? cmul(d, S.tw(2 * t)) : d;
+        }
+        __syncthreads();
+    }
     STAMP(0);
-    for (int i = 0; i < P.ns; ++i) {
-        if (P.rad[i] == 2) hb_radix2<false>(S, M, N, P.B[i], P.L[i]);
-        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<false, true>(S, M, N, P.B[i], 1, P.rad[i], S.pt + P.ptab[i]);
-        else if (P.mf[i]) hb_radixp_mfma<false, false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
-        else hb_radixp<false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
+    for (int i = r2 ? 1 : 0; i < P.ns; ++i) {
+        if (P.rad[i] == 2) hb_radix2<false>(S, P, i);
+        else if (P.rd[i]) hb_rader197<false>(S, P, S.pt + P.nptab);
+        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<false, true>(S, P, i, S.pt + P.ptab[i]);
+        else if (P.mf[i]) hb_radixp_mfma<false, false>(S, P, i, S.pt + P.ptab[i]);
+        else hb_radixp<false>(S, P, i, S.pt + P.ptab[i]);
         STAMP(i < 3 ? 1 + i : 3);
     }
     /* pointwise: pairs (k, M - k), k = 0 .. M/2 */
@@ -337,35 +488,69 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     }
     __syncthreads();
     STAMP(4);
-    for (int i = P.ns - 1; i >= 0; --i) {
-        if (P.rad[i] == 2) hb_radix2<true>(S, M, N, P.B[i], P.L[i]);
-        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<true, true>(S, M, N, P.B[i], 1, P.rad[i], S.pt + P.ptab[i]);
-        else if (P.mf[i]) hb_radixp_mfma<true, false>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
-        else hb_radixp<true>(S, M, N, P.B[i], P.L[i], P.rad[i], S.pt + P.ptab[i]);
+    for (int i = P.ns - 1; i >= (r2 ? 1 : 0); --i) {
+        if (P.rad[i] == 2) hb_radix2<true>(S, P, i);
+        else if (P.rd[i]) hb_rader197<true>(S, P, S.pt + P.nptab);
+        else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<true, true>(S, P, i, S.pt + P.ptab[i]);
+        else if (P.mf[i]) hb_radixp_mfma<true, false>(S, P, i, S.pt + P.ptab[i]);
+        else hb_radixp<true>(S, P, i, S.pt + P.ptab[i]);
     }
     STAMP(5);
     /* |analytic| = sqrt(y^2 + (c/N)^2), in place (two reals per complex slot) */
     const double inv = 1.0 / (double)N;
-    for (int m = threadIdx.x; m < M; m += HB_T) {
-        const double2 c = S.x[m], y = y2[m];
+    auto mag2 = [&](double2 c, double2 y) {
         const double i0 = c.x * inv, i1 = c.y * inv;
-        S.x[m] = make_double2(sqrt(y.x * y.x + i0 * i0), sqrt(y.y * y.y + i1 * i1));
+        return make_double2(sqrt(y.x * y.x + i0 * i0), sqrt(y.y * y.y + i1 * i1));
+    };
+    if (r2) {
+        for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIT radix 2 (conjugate twiddle before), then |.| */
+            const double2 ya = y2[t], yb = y2[t + H];
+            const double2 a = S.x[t];
+            double2 b = S.x[t + H];
+            if (t) b = cmulc(b, S.tw(2 * t));
+            S.x[t] = mag2(cadd(a, b), ya);
+            S.x[t + H] = mag2(csub(a, b), yb);
+        }
+    } else {
+        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = mag2(S.x[m], y2[m]);
     }
     __syncthreads();
     STAMP(6);
     /* centred rolling mean (min_periods 1): each thread a contiguous run of
      * outputs, the window sum slid along it (one direct sum per run) */
-    const double *mag = (const double *)S.x;
     const int64_t w = P.window;
     double *env = A.env + d0;
-    const int per = (N + HB_T - 1) / HB_T;                 /* <= HB_RMPER (host checks) */
+    const int per = P.per;                                 /* ceil(N / HB_T) <= HB_RMPER (host checks) */
+    const double *mag = (const double *)S.x;
     const int i0 = threadIdx.x * per, i1 = i0 + per < N ? i0 + per : N;
     double ev[HB_RMPER];
     /* full windows multiply by 1/w (within an ulp of the division; the
      * envelope's tolerance is 1e-9 relative), edge windows divide */
     const double invw = 1.0 / (double)w;
     auto mean = [&](double sum, int64_t cnt) { return cnt == w ? sum * invw : sum / (double)cnt; };
-    if (i0 < i1) {
+    int64_t sa, ea, sz, ez;
+    win_bounds(i0, N, w, sa, ea);
+    win_bounds(i1 - 1, N, w, sz, ez);
+    if (i0 < i1 && ez - ea == i1 - 1 - i0 && sz - sa == i1 - 1 - i0) {
+        /* both window ends slide by one per output: the same operations in
+         * the same order, with every LDS read issued before the sums */
+        const int cnt = i1 - i0;
+        double ad[HB_RMPER], sb[HB_RMPER];
+#pragma unroll
+        for (int j = 1; j < HB_RMPER; ++j)
+            if (j < cnt) { ad[j] = mag[ea + j - 1]; sb[j] = mag[sa + j - 1]; }
+        double sum = 0.0;
+        for (int64_t q = sa; q < ea; ++q) sum += mag[q];
+        const int64_t c = ea - sa;
+        ev[0] = mean(sum, c);
+#pragma unroll
+        for (int j = 1; j < HB_RMPER; ++j)
+            if (j < cnt) {
+                sum += ad[j];
+                sum -= sb[j];
+                ev[j] = mean(sum, c);
+            }
+    } else if (i0 < i1) {
         int64_t s, e;
         win_bounds(i0, N, w, s, e);
         double sum = 0.0;
@@ -399,7 +584,8 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
 
 /* ---------------------------------------------------------------------- */
 /* host: plan + tables (long double), cached per N */
-int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes, bool mfma) {
+int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes, bool mfma,
+                 bool rader) {
     if (nd < 4 || (nd & 1)) return 0;
     const int64_t M = nd / 2;
     int rad[HB_MAXS], ns = 0;
@@ -425,18 +611,29 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
     P->window = window;
     int64_t B = M;
     std::vector<int> primes;
+    if (M >= 16384) return 0;                 /* hb_div: dividends < 16 M, divisors <= M */
     for (int i = 0; i < ns; ++i) {
         const int r = rad[i];
         P->rad[i] = r;
         P->B[i] = (int32_t)B;
         P->L[i] = (int32_t)(B / r);
         B /= r;
+        const int h = (r - 1) / 2;
+        P->dL[i] = hb_magic((uint32_t)P->L[i]);
+        P->dP[i] = hb_magic((uint32_t)r);
+        P->dH[i] = hb_magic((uint32_t)(h > 0 ? h : 1));
+        P->dG[i] = hb_magic((uint32_t)((h + HB_KB) / HB_KB));
+        P->dT[i] = hb_magic((uint32_t)((h + 16) / 16));
         if (r > 2) {
             /* matrix-core form: 16 x 16 output tiles within the waves' budget */
             const int64_t units = ((M / r + 15) / 16) * (((r - 1) / 2 + 16) / 16);
             P->mf[i] = mfma && r >= HB_MF_PMIN && units <= (int64_t)(HB_T / 64) * HB_MF_UNITS;
+            /* Rader's 197-point DFT on the contiguous, twiddle-free stage */
+            P->rd[i] = rader && r == HB_RD_P && P->L[i] == 1;
+            if (P->rd[i]) P->mf[i] = 0;
             /* register-held outputs: (M / p) ceil((h + 1) / HB_KB) tasks over HB_T threads */
-            if (!P->mf[i] && (M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT) return 0;
+            if (!P->mf[i] && !P->rd[i] && (M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT)
+                return 0;
             int off = -1, acc = 0;
             for (int q : primes) { if (q == r) off = acc; acc += q; }
             if (off < 0) { off = acc; primes.push_back(r); }
@@ -448,10 +645,14 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
     int np = 0;
     for (int q : primes) np += q;
     P->nptab = np;
-    if ((nd + HB_T - 1) / HB_T > HB_RMPER) return 0;
-    *lds_bytes = (size_t)(M + P->ntwh + 128 + np) * sizeof(double2);
+    bool any_rd = false;
+    for (int i = 0; i < ns; ++i) any_rd = any_rd || P->rd[i];
+    P->nrtab = any_rd ? 2 * (HB_RD_P - 1) : 0;
+    P->per = (int32_t)((nd + HB_T - 1) / HB_T);
+    if (P->per > HB_RMPER) return 0;
+    *lds_bytes = (size_t)(M + P->ntwh + 128 + np + P->nrtab) * sizeof(double2);
     if (*lds_bytes > HB_LDS_MAX) return 0;
-    tabs->resize((size_t)P->ntwh + 128 + np);
+    tabs->resize((size_t)P->ntwh + 128 + np + P->nrtab);
     const long double tp = 6.283185307179586476925286766559005768L;
     for (int j = 0; j < P->ntwh; ++j) {
         const long double a = -tp * (long double)(128LL * j) / (long double)nd;
@@ -467,6 +668,25 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
             const long double a = tp * (long double)j / (long double)q;
             (*tabs)[o] = make_double2((double)cosl(a), (double)sinl(a));
         }
+    if (any_rd) {
+        /* Bh_k = DFT_196(b)_k / 196 with b_j = e^(-2 pi i (2^-j mod 197) / 197); then W_196^e */
+        constexpr int Q = HB_RD_P - 1;
+        int gi[Q];
+        for (int j = 0, e = 1; j < Q; ++j, e = (e * 99) % HB_RD_P) gi[j] = e;   /* 99 = 2^-1 mod 197 */
+        for (int k = 0; k < Q; ++k) {
+            long double re = 0.0L, im = 0.0L;
+            for (int j = 0; j < Q; ++j) {
+                const long double a = -tp * ((long double)gi[j] / HB_RD_P + (long double)((j * k) % Q) / Q);
+                re += cosl(a);
+                im += sinl(a);
+            }
+            (*tabs)[o + k] = make_double2((double)(re / Q), (double)(im / Q));
+        }
+        for (int e = 0; e < Q; ++e) {
+            const long double a = -tp * (long double)e / Q;
+            (*tabs)[o + Q + e] = make_double2((double)cosl(a), (double)sinl(a));
+        }
+    }
     return 1;
 }
 

@@ -3,8 +3,8 @@
  * thread 0 of each workgroup): load | fwd stage 0 | 1 | 2 | pointwise | inverse | |z| | rolling mean.
  *   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/hbench.hip -o tools/hbench
  *   ./tools/hbench [files] [nd]
- * Runs the plan with and without the matrix-core odd-prime stage and prints
- * the largest envelope difference between the two (relative to max |env|).
+ * Runs the plan with the direct, matrix-core and Rader odd-prime stages and
+ * prints the largest envelope differences (relative to max |env|).
  */
 #define BPMX_STAMPS 1
 #include "../bpm_analysis_amd/csrc/k_hilbert.hip"
@@ -15,13 +15,13 @@
 using namespace bpmx;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-static double run(int F, int64_t nd, bool mfma, std::vector<double> &y, std::vector<double> &env_out) {
+static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> &y, std::vector<double> &env_out) {
     HilbPlan P;
     std::vector<double2> tabs;
     size_t lds = 0;
-    if (!hilbert_plan(nd, 30, &P, &tabs, &lds, mfma)) { printf("no plan\n"); exit(1); }
+    if (!hilbert_plan(nd, 30, &P, &tabs, &lds, mfma, rader)) { printf("no plan\n"); exit(1); }
     printf("nd %lld M %d stages", (long long)nd, P.M);
-    for (int i = 0; i < P.ns; ++i) printf(" %d%s", P.rad[i], P.mf[i] ? "(mfma)" : "");
+    for (int i = 0; i < P.ns; ++i) printf(" %d%s", P.rad[i], P.mf[i] ? "(mfma)" : P.rd[i] ? "(rader)" : "");
     printf(" lds %zu\n", lds);
     std::vector<int64_t> doff(F + 1);
     for (int f = 0; f <= F; ++f) doff[f] = (int64_t)f * nd;
@@ -69,11 +69,17 @@ int main(int argc, char **argv) {
     std::vector<double> y((size_t)F * nd);
     unsigned long long s = 1;
     for (auto &v : y) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (double)(s >> 11) / 9007199254740992.0 - 0.5; }
-    std::vector<double> e0, e1;
-    run(F, nd, false, y, e0);
-    run(F, nd, true, y, e1);
-    double mx = 0, d = 0;
-    for (size_t i = 0; i < e0.size(); ++i) { mx = fmax(mx, fabs(e0[i])); d = fmax(d, fabs(e0[i] - e1[i])); }
-    printf("max |env_direct - env_mfma| / max|env| = %.3e\n", d / mx);
+    std::vector<double> e0, e1, e2;
+    run(F, nd, false, false, y, e0);
+    run(F, nd, true, false, y, e1);
+    run(F, nd, true, true, y, e2);
+    double mx = 0, d = 0, d2 = 0;
+    for (size_t i = 0; i < e0.size(); ++i) {
+        mx = fmax(mx, fabs(e0[i]));
+        d = fmax(d, fabs(e0[i] - e1[i]));
+        d2 = fmax(d2, fabs(e0[i] - e2[i]));
+    }
+    printf("max |env_direct - env_mfma| / max|env| = %.3e, max |env_direct - env_rader| / max|env| = %.3e\n", d / mx,
+           d2 / mx);
     return 0;
 }
