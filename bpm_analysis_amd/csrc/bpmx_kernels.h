@@ -271,6 +271,11 @@ constexpr int WM_PMAX = 12288;               /* kept samples of the pruned varia
 struct WmLayout {
     size_t tab, meta, kpos, area, total;
 };
+/* pruned variant's per-64 tables (NBK entries each): upper side mask 8, prefix
+ * 4, thr 1, b* levels 9; lower side (8-aligned) the same with a* levels */
+constexpr int WM_NBK = WM_MMAX / 64 + 2;
+constexpr int WM_META_LOW = (WM_NBK * 22 + 7) & ~7;
+constexpr int WM_META_B = WM_META_LOW + WM_NBK * 22;
 __host__ __device__ inline size_t wm_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline WmLayout wm_layout(int64_t nmax, bool prune) {
     const int64_t n = nmax < 1 ? 1 : (nmax > WM_MMAX ? WM_MMAX : nmax);
@@ -287,7 +292,7 @@ __host__ __device__ inline WmLayout wm_layout(int64_t nmax, bool prune) {
     WmLayout l;
     l.tab = 0;
     l.meta = wm_align16((size_t)WM_TRMAX * (prune ? 20 : 12) + (size_t)NBK * 4);
-    l.kpos = wm_align16(l.meta + (prune ? (size_t)NBK * 22 : 0));   /* mask 8, prefix 4, thr 1, b* levels 9 */
+    l.kpos = wm_align16(l.meta + (prune ? (size_t)WM_META_B : 0));
     l.area = wm_align16(l.kpos + (prune ? (size_t)m * 2 : 0));
     l.total = l.area + (size_t)area;
     return l;

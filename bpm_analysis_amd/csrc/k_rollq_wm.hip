@@ -13,8 +13,16 @@
  *      b* of every block whose windows can contain it is strictly greater than
  *      each such window's (k+1)-th smallest, so dropping it changes no output;
  *      the window's k-th smallest is the k-th smallest of its kept samples.
+ *      The lower side likewise: a* = the bin of the k_min-th smallest of the
+ *      position blocks covering the block's windows' union bounds every one of
+ *      its windows' k-th smallest from below, so a sample below a* of every
+ *      block whose windows can contain it ranks before the window's k-th and
+ *      (k+1)-th smallest; such samples are only counted (a second mask +
+ *      prefix), and the window's k-th smallest is the (k - low count)-th of its
+ *      kept samples.
  *      Kept samples are compacted (a per-64 bit mask + prefix maps a position
- *      range to a kept range).  On the metric workload ~30 % are kept.
+ *      range to a kept range).  On the metric workload ~19 % are kept (31 %
+ *      with the upper bound alone, tools/prune_sim.py).
  *      Recordings keeping more than WM_PMAX take the unpruned variant.
  *   1. ranks: the kept samples are ordered by (value, index) with an LSD radix
  *      sort on order-preserving 64-bit keys, 8-bit digits, digits constant
@@ -149,6 +157,11 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
     int32_t *kpre = (int32_t *)(kmask + (WM_MMAX / 64 + 2)); /* [NPB + 1] kept before the block */
     uint8_t *thr = (uint8_t *)(kpre + (WM_MMAX / 64 + 2));   /* [NPB] highest bin kept */
     uint8_t *bstar = thr + (WM_MMAX / 64 + 2);               /* [9][n/64] per output block, then sparse-table maxima */
+    /* the lower side: samples below every reachable window's k-th smallest */
+    uint64_t *lmask = (uint64_t *)(smem + Lay.meta + WM_META_LOW);         /* [NPB + 1] low bits */
+    int32_t *lpre = (int32_t *)(lmask + (WM_MMAX / 64 + 2)); /* [NPB + 1] low samples before the block */
+    uint8_t *lthr = (uint8_t *)(lpre + (WM_MMAX / 64 + 2));  /* [NPB] lowest bin kept */
+    uint8_t *astar = lthr + (WM_MMAX / 64 + 2);              /* [9][n/64] per output block, then sparse-table minima */
     uint16_t *kpos = (uint16_t *)(smem + Lay.kpos);          /* kept index -> position - t0 */
     int m = mall;
     if (PRUNE) {
@@ -265,6 +278,28 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
                 bs = lo;
             }
             bstar[B] = (uint8_t)bs;
+            /* a*: the bin of the k_min-th smallest of the position blocks
+             * covering the block's windows' union (a superset of every window,
+             * so that sample is at most each window's k-th smallest; k_min from
+             * the fewest observations, at an end of the block: nobs is unimodal).
+             * A sample in a lower bin is strictly below every such window's k-th
+             * smallest: it leaves the structure and is only counted. */
+            const int64_t nl = e0 - (s0 > t0 ? s0 : t0), nr = e1 - (s1 > t0 ? s1 : t0);
+            const int64_t nmin = nl < nr ? nl : nr;
+            const int kmin = nmin > 1 ? (int)(int64_t)(q * (double)(nmin - 1)) : 0;
+            const int64_t ulo = (s0 > t0 ? s0 : t0) - t0, uhi = e1 - t0;   /* union, relative */
+            const int cbs = ulo > 0 ? (int)(ulo >> 6) : 0;
+            const int cbe = uhi > 0 ? min(NPB, (int)((uhi + 63) >> 6)) : 0;
+            int as = 0;
+            if (cbe > cbs && nmin > 0 && (int)hist[cbe * NB + NB - 1] - (int)hist[cbs * NB + NB - 1] >= kmin + 1) {
+                int lo = 0, hi = NB - 1;                     /* count(<= hi) reaches k_min + 1 */
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if ((int)hist[cbe * NB + mid] - (int)hist[cbs * NB + mid] >= kmin + 1) hi = mid; else lo = mid + 1;
+                }
+                as = lo;
+            }
+            astar[B] = (uint8_t)as;
         }
         __syncthreads();
         /* sparse table of b* maxima over 2^j consecutive blocks, j = 1 .. 8 */
@@ -272,10 +307,14 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
             const uint8_t *src = bstar + (size_t)(j - 1) * (WM_MMAX / 64 + 2);
             uint8_t *dst = bstar + (size_t)j * (WM_MMAX / 64 + 2);
             for (int B = tid; B + (1 << j) <= NBO; B += WM_T) dst[B] = max(src[B], src[B + (1 << (j - 1))]);
+            const uint8_t *asrc = astar + (size_t)(j - 1) * (WM_MMAX / 64 + 2);
+            uint8_t *adst = astar + (size_t)j * (WM_MMAX / 64 + 2);
+            for (int B = tid; B + (1 << j) <= NBO; B += WM_T) adst[B] = min(asrc[B], asrc[B + (1 << (j - 1))]);
             __syncthreads();
         }
         STAMP(11);
-        /* highest b* over the output blocks whose windows can reach a position block */
+        /* highest b* and lowest a* over the output blocks whose windows can
+         * reach a position block */
         const int64_t off = (W - 1) / 2;
         for (int pb = tid; pb < NPB; pb += WM_T) {
             const int64_t a = t0 + ((int64_t)pb << 6);
@@ -286,34 +325,44 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
             const int j = 31 - __clz(len);
             const uint8_t *st = bstar + (size_t)j * (WM_MMAX / 64 + 2);
             thr[pb] = max(st[B0], st[B1 - (1 << j) + 1]);
+            const uint8_t *sa = astar + (size_t)j * (WM_MMAX / 64 + 2);
+            lthr[pb] = min(sa[B0], sa[B1 - (1 << j) + 1]);
         }
         __syncthreads();
         STAMP(12);
-        /* keep masks, one 64-sample block per wave step */
+        /* keep and low masks, one 64-sample block per wave step */
         int kc = 0;
         for (int pb = wid; pb < NPB; pb += NWV) {
             const int p = (pb << 6) + lane;
-            const bool keep = p < mall && (int)bin8[p] <= (int)thr[pb];
-            const uint64_t bal = __ballot(keep);
-            if (lane == 0) kmask[pb] = bal;
+            const int b = p < mall ? (int)bin8[p] : -1;
+            const bool low = p < mall && b < (int)lthr[pb];
+            const bool keep = p < mall && !low && b <= (int)thr[pb];
+            const uint64_t bal = __ballot(keep), lbal = __ballot(low);
+            if (lane == 0) { kmask[pb] = bal; lmask[pb] = lbal; }
         }
-        if (tid == 0) kmask[NPB] = 0ull;
+        if (tid == 0) { kmask[NPB] = 0ull; lmask[NPB] = 0ull; }
         __syncthreads();
-        /* exclusive prefix of kept counts over blocks (NPB <= 289: one wave) */
-        if (wid == 0) {
+        /* exclusive prefixes of kept (wave 0) and low (wave 1) counts over
+         * blocks (NPB <= 289) */
+        if (wid < 2) {
+            const uint64_t *msk = wid ? lmask : kmask;
+            int32_t *pre = wid ? lpre : kpre;
             int run = 0;
             for (int base = 0; base < NPB; base += 64) {
                 const int pb = base + lane;
-                const int v = pb < NPB ? __popcll(kmask[pb]) : 0;
+                const int v = pb < NPB ? __popcll(msk[pb]) : 0;
                 int x = v;
                 for (int o = 1; o < 64; o <<= 1) {
                     const int y = __shfl_up(x, o);
                     if (lane >= o) x += y;
                 }
-                if (pb < NPB) kpre[pb] = run + x - v;
+                if (pb < NPB) pre[pb] = run + x - v;
                 run += __shfl(x, 63);
             }
-            if (lane == 0) { kpre[NPB] = run; s_mk = run; }
+            if (lane == 0) {
+                pre[NPB] = run;
+                if (!wid) s_mk = run;
+            }
         }
         __syncthreads();
         kc = s_mk;
@@ -337,6 +386,11 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         if (!PRUNE) return p;
         const uint64_t mk = kmask[p >> 6];
         return kpre[p >> 6] + __popcll(mk & ((1ull << (p & 63)) - 1ull));
+    };
+    /* samples below the structure among relative positions [0, p) */
+    auto lidx = [&](int p) -> int {
+        const uint64_t mk = lmask[p >> 6];
+        return lpre[p >> 6] + __popcll(mk & ((1ull << (p & 63)) - 1ull));
     };
     STAMP(7);
 
@@ -569,7 +623,8 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
                 k = (int64_t)idxf;
             }
             const bool interp = !(nobs == 1 || (double)k == idxf);
-            const int ra = kth(plo, phi, (int)k);
+            /* the window's samples below the structure rank before every kept one */
+            const int ra = kth(plo, phi, (int)k - (PRUNE ? lidx((int)(e - t0)) - lidx((int)(lo - t0)) : 0));
             const double va = svl ? svl[ra] : dval(t0 + spos(posR[ra]));
             if (!interp) {
                 res = va;
