@@ -738,3 +738,41 @@ def test_run_sharded_single_rank_on_the_gpu(det, tmp_path):
         a = B.analyze_recording(o["env"], o["sr"], o["floor"], o["troughs"], o["peaks"], params)
         assert _same(r["final_peaks"], a["final_peaks"])
         np.testing.assert_allclose(r["bpm"], a["final_metrics"]["smoothed_bpm"].values, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_quantile_kernel_paths(det):
+    """k_quantile_reg: the bin-gather fast path, its radix-select fallback (a
+    bin with more than 512 keys: long runs of tied values), a constant
+    envelope (no varying key bit) and the q = 0 / 1 ends, through the static
+    noise floor of envelopes without troughs (floor = np.quantile(env, q),
+    bpm_analysis.py:1075) and against the oracle's troughs and peaks."""
+    from bpm_analysis_amd import _native as N
+    rng = np.random.default_rng(11)
+    n = 18124
+    envs = {
+        "smooth": np.sort(np.abs(rng.normal(300.0, 80.0, n))),
+        "wide_range": np.sort(np.exp(rng.uniform(-12.0, 9.0, n))),
+        "ties": np.sort(np.repeat(rng.uniform(1.0, 2.0, 24), (n + 23) // 24)[:n]),
+        "constant": np.full(n, 7.25),
+        "short": np.sort(rng.uniform(0.0, 1.0, 41)),
+    }
+    for q in (0.0, 0.2, 0.5, 0.999, 1.0):
+        params = dict(G.BASE_PARAMS)
+        params["noise_floor_quantile"] = q
+        got = det.run_env_host(list(envs.values()), 302, params, N.STAGE_FLOOR)
+        for (name, env), r in zip(envs.items(), got):
+            want = np.quantile(env, q)
+            assert np.all(r["floor"] == want), (name, q, r["floor"][:3], want)
+    # the prominence quantiles (0.1 of the envelope) on bumpy envelopes
+    params = dict(G.BASE_PARAMS)
+    t = np.arange(n)
+    bumpy = [np.abs(np.sin(t / 37.0)) * 100 + np.round(rng.uniform(0, 3, n)),      # many ties
+             np.abs(np.sin(t / 23.0)) * np.exp(rng.uniform(-6, 6, n))]
+    got = det.run_env_host(bumpy, 302, params, N.STAGE_FLOOR | N.STAGE_PEAKS)
+    d = O.derive(302, params)
+    for env, r in zip(bumpy, got):
+        of, ot, _ = O.noise_floor(env, d, params)
+        assert _same(r["troughs"], ot)
+        assert _same(r["floor"], of)
+        assert _same(r["peaks"], O.raw_peaks(env, of, d, params))
