@@ -579,6 +579,9 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
          * tile, wait for everything. */
         if (NM_SLOTS == 2 && t + stride < A.n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NM_NDMA) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        /* the slot is the scarce resource: its reader runs ahead of the other
+         * waves' epilogues until the refill is issued */
+        __builtin_amdgcn_s_setprio(2);
         const int coff = (int)(tl.s0 & 7);
         {
             const int64_t a0 = tl.s0 - coff, tail0 = total & ~(int64_t)7;
@@ -632,6 +635,7 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
          * the next one (one slot: it flies during this epilogue) */
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (tr < A.n_tiles) dma(tn.s0, slot);
+        __builtin_amdgcn_s_setprio(0);
         /* lane half 0 holds even coefficients, half 1 odd ones; N tile n = blocks 32n.. */
         double cf[8];
 #pragma unroll
