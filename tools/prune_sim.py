@@ -1,7 +1,9 @@
 """Simulate the value-bin pruning of the final-floor rolling quantile on
 synthetic recordings: fraction of the curve's samples that can ever be a
 window's k-th or (k+1)-th smallest (exact bound, 64 value bins, 64-output
-blocks).  Host-only study tool."""
+blocks).  Prints the upper bound alone (b*) and both sides (b* and a*, the
+bin of the k_min-th smallest of a block's windows' union: samples below it
+are only counted).  Host-only study tool."""
 import sys, os
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -21,27 +23,36 @@ def keep_fraction(dense, t0, W, q, nbins=NB, blk=64):
     off = (W - 1) // 2
     nbk = (n + blk - 1) // blk
     bstar = np.full(nbk, nbins - 1)
+    astar = np.zeros(nbk, np.int64)
     for B in range(nbk):
         i0, i1 = B * blk, min(n, B * blk + blk) - 1
         e0 = min(i0 + 1 + off, n); s1 = max(min(i1 + 1 + off, n) - W, 0)
+        s0 = max(e0 - W, 0); e1 = min(i1 + 1 + off, n)
         lo, hi = max(s1, t0), e0            # intersection of the block's windows
-        kmax = 0
+        kq = []
         for i in (i0, i1):
             e = min(i + 1 + off, n); s = max(e - W, 0); nobs = e - max(s, t0)
-            kmax = max(kmax, int(q * (nobs - 1)) if nobs > 1 else 0)
-        if hi - lo < kmax + 2:
-            continue
-        c = np.cumsum(np.bincount(bins[lo:hi], minlength=nbins))
-        bstar[B] = int(np.searchsorted(c, kmax + 2))
-    # threshold per position: max over blocks whose union window contains it
-    keep = np.zeros(n, bool)
+            kq.append(int(q * (nobs - 1)) if nobs > 1 else 0)
+        kmax, kmin = max(kq), min(kq)
+        if hi - lo >= kmax + 2:
+            c = np.cumsum(np.bincount(bins[lo:hi], minlength=nbins))
+            bstar[B] = int(np.searchsorted(c, kmax + 2))
+        ulo, uhi = max(s0, t0), e1          # union of the block's windows
+        if uhi > ulo:
+            cu = np.cumsum(np.bincount(bins[ulo:uhi], minlength=nbins))
+            if cu[-1] >= kmin + 1:
+                astar[B] = int(np.searchsorted(cu, kmin + 1))
+    # thresholds per position: over the blocks whose union window contains it
     thr = np.full(n, -1)
+    lthr = np.full(n, nbins)
     for B in range(nbk):
         i0, i1 = B * blk, min(n, B * blk + blk) - 1
         s0 = max(min(i0 + 1 + off, n) - W, 0); e1 = min(i1 + 1 + off, n)
         thr[s0:e1] = np.maximum(thr[s0:e1], bstar[B])
-    keep[t0:] = bins[t0:] <= thr[t0:]
-    return keep[t0:].mean()
+        lthr[s0:e1] = np.minimum(lthr[s0:e1], astar[B])
+    b = bins[t0:]
+    upper = b <= thr[t0:]
+    return upper.mean(), (upper & (b >= lthr[t0:])).mean()
 
 
 p = dict(DEFAULT_PARAMS)
@@ -53,5 +64,5 @@ for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     floor, tr, flags = O.noise_floor(env, d, p)
     dense = O.interp_dense(tr, env)
     fr.append(keep_fraction(dense, int(tr[0]), d.noise_window, p["noise_floor_quantile"]))
-    print(seed, len(tr), round(fr[-1], 3))
-print("mean keep", np.mean(fr))
+    print(seed, len(tr), "upper bound %.3f, both sides %.3f" % fr[-1])
+print("mean keep (upper, both sides)", np.mean(fr, axis=0))
