@@ -499,6 +499,29 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         if (rc != BPMX_OK) return rc;
         const int64_t wm_n = std::min<int64_t>(maxnd, WM_MMAX);
         const size_t wm_lds_p = wm_layout(wm_n, true).total, wm_lds = wm_layout(wm_n, false).total;
+        /* long recordings: the pruned wavelet matrix over chunks of wm_c outputs
+         * (a chunk's windows reach wm_c + W - 1 samples); a recording with a
+         * chunk it cannot take falls to the sorted-union kernel */
+        const int64_t wm_c = (WM_MMAX - W + 1) / 64 * 64;
+        const bool wm_chunks = use_wm && maxnd > WM_MMAX && !(P->options & BPMX_OPT_ROLLQ_NOPRUNE) && wm_c >= 2048;
+        const int64_t wm_nch = wm_chunks ? (maxnd + wm_c - 1) / wm_c : 1;
+        int32_t *wm_fail = wm_chunks ? (int32_t *)ctx->buf("wm_fail", (size_t)F * 4, &rc) : nullptr;
+        uint16_t *wm_pos_ch = wm_chunks ? (uint16_t *)ctx->buf("wm_pos_ch", (size_t)F * wm_nch * WM_PMAX * 2, &rc) : nullptr;
+        if (rc != BPMX_OK) return rc;
+        if (wm_nch > 65535) return fail(BPMX_E_LIMIT, "recording too long for the chunked rolling quantile");
+        /* k_interp / k_floor_final stride over a recording with gx workgroups:
+         * 8, or more when the batch has few recordings */
+        const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, std::max<int64_t>(8, 2048 / F)), F);
+        /* dense = np.interp of the troughs, for the recordings the rolling-quantile
+         * kernels do not interpolate themselves (the wavelet matrix stages up to
+         * WM_TRMAX troughs, or a long recording's chunk) */
+        auto interp = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, int64_t skip_gt) -> int {
+            InterpArgs a;
+            a.env = O->env; a.doff = d_doff; a.troughs = tr; a.ntr = ntr; a.run = run; a.n_files = F;
+            a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1; a.skip_gt = skip_gt;
+            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
+            return BPMX_OK;
+        };
         auto rollq = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, double *outp,
                          int32_t *allnan) -> int {
             RollqArgs a;
@@ -506,6 +529,21 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.env = O->env; a.ntr = ntr;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
             a.out = outp; a.allnan = allnan; a.wm_max = use_wm ? WM_MMAX : 0;
+            a.wm_chunk = 0; a.wm_fail = wm_fail; a.wm_pos_ch = wm_pos_ch;
+            int rq_rc = BPMX_OK;
+            int32_t *vfl = need_merge ? (int32_t *)ctx->buf("rollq_valid", (size_t)F * 8, &rq_rc) : nullptr;
+            if (rq_rc != BPMX_OK) return rq_rc;
+            a.vfirst = vfl;
+            a.vlast = vfl ? vfl + F : nullptr;
+            if (need_merge) {
+                HIP_TRY(hipMemsetAsync(a.vfirst, 0x7F, (size_t)F * 4, s));      /* 0x7F7F7F7F: above any index */
+                HIP_TRY(hipMemsetAsync(a.vlast, 0xFF, (size_t)F * 4, s));       /* -1 */
+            }
+            if (wm_chunks) {
+                HIP_TRY(hipMemsetAsync(wm_fail, 0, (size_t)F * 4, s));
+                a.wm_chunk = (int32_t)wm_c;
+            }
+            if ((rq_rc = interp(run, tr, ntr, wm_chunks ? WM_MMAX : INT64_MAX)) != BPMX_OK) return rq_rc;
             if (use_wm) {
                 /* pruned structure first; recordings it cannot take (too many
                  * kept samples, > WM_TRMAX troughs) are flagged in wm_full for
@@ -514,9 +552,10 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
                 if (!(P->options & BPMX_OPT_ROLLQ_NOPRUNE)) {
                     (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds_p);
-                    LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F), dim3(WM_T), wm_lds_p, s, a, wm_pos,
-                           wm_full);
+                    LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F, (unsigned)wm_nch), dim3(WM_T), wm_lds_p, s, a,
+                           wm_pos, wm_full);
                     b.run = wm_full;
+                    b.wm_chunk = 0;
                 }
                 (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds);
@@ -525,12 +564,13 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             }
             if (!need_merge) return BPMX_OK;
             /* long recordings: a workgroup per chunk of outputs (each chunk pays
-             * one extra window fill: ~13 merge rounds against 32 or 16 tiles) */
-            int rq_rc = BPMX_OK;
-            int32_t *vfl = (int32_t *)ctx->buf("rollq_valid", (size_t)F * 8, &rq_rc);
-            if (rq_rc != BPMX_OK) return rq_rc;
-            a.vfirst = vfl;
-            a.vlast = vfl + F;
+             * one extra window fill: ~13 merge rounds against 32 or 16 tiles);
+             * after the chunked wavelet matrix only the recordings it gave up */
+            RollqArgs fill = a;
+            if (wm_chunks) {
+                a.run = wm_fail;
+                if ((rq_rc = interp(wm_fail, tr, ntr, INT64_MAX)) != BPMX_OK) return rq_rc;
+            }
             /* 8192 outputs per chunk, halved (down to 1024) while the batch
              * gives fewer than 1024 workgroups: a chunk's first-window fill is
              * fixed overhead, worth paying only when CUs would sit idle */
@@ -540,8 +580,6 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             if (merge_g) a.chunk = std::max<int64_t>(a.chunk, (W + RQ_T - 1) / RQ_T * RQ_T);
             const int64_t nch = (maxnd + a.chunk - 1) / a.chunk;
             if (nch > 65535) return fail(BPMX_E_LIMIT, "recording too long for the chunked rolling quantile");
-            HIP_TRY(hipMemsetAsync(a.vfirst, 0x7F, (size_t)F * 4, s));      /* 0x7F7F7F7F: above any index */
-            HIP_TRY(hipMemsetAsync(a.vlast, 0xFF, (size_t)F * 4, s));       /* -1 */
             const dim3 gq((unsigned)F, (unsigned)nch);
             if (merge_g) {
                 a.gcap = gcap;
@@ -560,20 +598,11 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 LAUNCH(ctx, s, "k_rolling_quantile", (k_rolling_quantile<RQ_T, 32>), gq, dim3(RQ_T), lds, s, a);
             }
-            LAUNCH(ctx, s, "k_rollq_fill", k_rollq_fill, dim3(4, (unsigned)F), dim3(256), 0, s, a);
+            LAUNCH(ctx, s, "k_rollq_fill", k_rollq_fill, dim3(4, (unsigned)F), dim3(256), 0, s, fill);
             return BPMX_OK;
         };
-        /* k_interp / k_floor_final stride over a recording with gx workgroups:
-         * 8, or more when the batch has few recordings */
-        const dim3 g2((unsigned)std::min<int64_t>((maxnd + 255) / 256, std::max<int64_t>(8, 2048 / F)), F);
         if (O->n_raw_troughs)
             HIP_TRY(hipMemcpyAsync(O->n_raw_troughs, d_nraw, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
-        {
-            InterpArgs a;
-            a.env = O->env; a.doff = d_doff; a.troughs = rawt; a.ntr = d_nraw; a.run = d_run1; a.n_files = F;
-            a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1;
-            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
-        }
         /* Draft floor: sanitize reads it at the raw troughs only, so the
          * recordings whose every keep decision follows from k_draft_bounds'
          * bracket skip the full rolling quantile; the others (and, after
@@ -608,12 +637,6 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             LAUNCH(ctx, s, "k_sanitize", k_sanitize, dim3(F), dim3(256), 0, s, a);
         }
         if (bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
-        {
-            InterpArgs a;
-            a.env = O->env; a.doff = d_doff; a.troughs = O->troughs; a.ntr = O->n_troughs; a.run = d_run2;
-            a.n_files = F; a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1;
-            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
-        }
         if ((rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2)) != BPMX_OK) return rc;
         {
             FinalArgs a;

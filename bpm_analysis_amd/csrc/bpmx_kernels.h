@@ -153,6 +153,7 @@ struct InterpArgs {
     int32_t n_files;
     double *dense;
     int64_t skip_n;          /* skip files with n <= skip_n and <= WM_TRMAX troughs (k_rollq_wm interpolates) */
+    int64_t skip_gt;         /* skip files with n > skip_gt (the chunked k_rollq_wm interpolates those) */
 };
 
 struct RollqArgs {
@@ -172,6 +173,13 @@ struct RollqArgs {
     double *gv;              /* k_rolling_quantile_g: per-workgroup union scratch, 2 x gcap values ... */
     int32_t *gp;             /* ... and 2 x gcap positions */
     int64_t gcap;
+    /* k_rollq_wm_t<true> over chunks of long recordings (n > WM_MMAX): wm_chunk
+     * outputs per workgroup (blockIdx.y = chunk, 0 = off), each chunk's kept
+     * positions in wm_pos_ch (WM_PMAX per chunk); a chunk it cannot take sets
+     * wm_fail[f] and the recording goes to k_rolling_quantile */
+    int32_t wm_chunk;
+    int32_t *wm_fail;
+    uint16_t *wm_pos_ch;
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif

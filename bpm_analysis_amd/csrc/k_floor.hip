@@ -37,6 +37,7 @@ __global__ __launch_bounds__(256) void k_interp(InterpArgs A) {
     if (f >= A.n_files || !A.run[f]) return;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     if (n <= A.skip_n && A.ntr[f] <= WM_TRMAX) return;      /* k_rollq_wm interpolates these itself */
+    if (n > A.skip_gt) return;
     const int64_t *t = A.troughs + d0;
     const double *e = A.env + d0;
     /* a few workgroups per recording striding over it: a recording the

@@ -85,9 +85,48 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         return;
     }
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
-    const int ntr = A.env ? A.ntr[f] : 0;
+    const int ntr_all = A.env ? A.ntr[f] : 0;
+    /* chunk mode: a long recording's outputs [o0, o1) in workgroup (f, chunk),
+     * over the samples [t0, top) their windows reach */
+    const bool chunked = PRUNE && A.wm_chunk > 0 && n > WM_MMAX && A.env;
+    if (!chunked && blockIdx.y > 0) return;
+    const int64_t W = A.window, minp = A.min_periods;
+    int64_t o0 = 0, o1 = n, t0 = 0, top = n;
+    int jlo = 0, ntr = ntr_all;                              /* troughs staged: [jlo, jlo + ntr) */
+    __shared__ int s_jlo, s_jhi;
+    if (chunked) {
+        if (tid == 0 && blockIdx.y == 0) full[f] = 0;        /* long: never the unpruned variant */
+        o0 = (int64_t)blockIdx.y * A.wm_chunk;
+        if (o0 >= n) return;
+        o1 = min<int64_t>(n, o0 + A.wm_chunk);
+        int64_t s, e;
+        win_bounds(o0, n, W, s, e);
+        const int64_t *tr = A.troughs + d0;
+        t0 = s > tr[0] ? s : tr[0];                          /* every chunk window lies in [t0, top) */
+        win_bounds(o1 - 1, n, W, s, e);
+        top = e;
+        if (tid == 0) {                                      /* last trough <= t0, first trough >= top - 1 */
+            int lo = 0, hi = ntr_all;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (tr[mid] <= t0) lo = mid + 1; else hi = mid; }
+            s_jlo = lo > 0 ? lo - 1 : 0;
+            lo = 0; hi = ntr_all;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (tr[mid] < top - 1) lo = mid + 1; else hi = mid; }
+            s_jhi = lo < ntr_all ? lo : ntr_all - 1;
+        }
+        __syncthreads();
+        jlo = s_jlo;
+        ntr = s_jhi - s_jlo + 1;
+        if (top <= t0) {                                     /* no finite sample in reach: NaN outputs */
+            for (int64_t i = o0 + tid; i < o1; i += WM_T) A.out[d0 + i] = __builtin_nan("");
+            return;
+        }
+        if (top - t0 > WM_MMAX || ntr > WM_TRMAX) {
+            if (tid == 0) A.wm_fail[f] = 1;
+            return;
+        }
+    }
     const bool fused = A.env && ntr <= WM_TRMAX;
-    if (n > WM_MMAX || n <= 0 || (PRUNE && !fused)) {        /* k_rolling_quantile / the unpruned variant */
+    if (!chunked && (n > WM_MMAX || n <= 0 || (PRUNE && !fused))) {   /* k_rolling_quantile / the unpruned variant */
         if (PRUNE && tid == 0) full[f] = (n <= WM_MMAX && n > 0) ? 1 : 0;
         return;
     }
@@ -98,10 +137,11 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
 
     const double *dense = A.dense + d0;
     double *out = A.out + d0;
-    uint16_t *ps = pos_scratch + d0;                         /* kept index of each rank */
-    const int64_t t0 = A.troughs[d0];
-    const int mall = (int)(n - t0);                          /* finite samples dense[t0:n) */
-    const WmLayout Lay = wm_layout(n, PRUNE);
+    /* kept index of each rank */
+    uint16_t *ps = chunked ? A.wm_pos_ch + ((int64_t)f * gridDim.y + blockIdx.y) * WM_PMAX : pos_scratch + d0;
+    if (!chunked) t0 = A.troughs[d0];
+    const int mall = (int)(top - t0);                        /* finite samples dense[t0:top) */
+    const WmLayout Lay = wm_layout(chunked ? top - t0 : n, PRUNE);
     if (tid == 0) { s_first = INT_MAX; s_last = -1; }
     STAMP_DECL
 
@@ -110,17 +150,18 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
     double *s_tv = (double *)(smem + Lay.tab);
     double *s_sl = s_tv + WM_TRMAX;                          /* per-segment slope (pruned variant) */
     int32_t *s_tp = (int32_t *)(s_sl + (PRUNE ? WM_TRMAX : 0));
-    int32_t *s_bj = s_tp + WM_TRMAX;                         /* [n/64 + 1]: last trough <= block start */
+    int32_t *s_bj = s_tp + WM_TRMAX;                         /* [(top - xb)/64 + 1]: last trough <= block start */
+    const int64_t xb = chunked ? t0 : 0;                     /* block table origin */
     if (fused) {
-        const int64_t *tr = A.troughs + d0;
+        const int64_t *tr = A.troughs + d0 + jlo;
         for (int j = tid; j < ntr; j += WM_T) {
             s_tp[j] = (int32_t)tr[j];
             s_tv[j] = A.env[d0 + tr[j]];
         }
         __syncthreads();
-        for (int64_t b = tid; b <= (n >> 6); b += WM_T) {
+        for (int64_t b = tid; b <= ((top - xb) >> 6); b += WM_T) {
             int lo = 0, hi = ntr;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= (b << 6)) lo = mid + 1; else hi = mid; }
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid] <= xb + (b << 6)) lo = mid + 1; else hi = mid; }
             s_bj[b] = lo - 1;
         }
         if (PRUNE) {
@@ -130,11 +171,13 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         }
         __syncthreads();
     }
-    /* interp_at's arithmetic, with the bracketing trough found from the block table */
+    /* interp_at's arithmetic, with the bracketing trough found from the block
+     * table (a staged run that stops before the recording's last trough always
+     * reaches past every position asked for) */
     auto dval = [&](int64_t x) -> double {
         if (!fused) return dense[x];
         if (ntr == 0 || x < s_tp[0]) return __builtin_nan("");
-        int j = s_bj[x >> 6];
+        int j = s_bj[(x - xb) >> 6];
         if (j < 0) j = 0;
         while (j + 1 < ntr && s_tp[j + 1] <= x) ++j;
         if (j == ntr - 1 || s_tp[j] == x) return s_tv[j];
@@ -148,7 +191,6 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         return r;
     };
 
-    const int64_t W = A.window, minp = A.min_periods;
     const double q = A.q;
 
     /* ---------------- 0. pruning (PRUNE only) ---------------- */
@@ -192,7 +234,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         const double vmin = s_vmin, span = s_vmax - s_vmin;
         const bool ok = span == span && span < __builtin_inf();
         if (!ok) {                                           /* non-finite curve: no pruning */
-            if (tid == 0) full[f] = 1;
+            if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
             return;
         }
         const double scale = span > 0.0 ? (double)NB / span : 0.0;
@@ -256,9 +298,9 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         /* b* per block of 64 outputs, one thread per block: the lowest bin
          * with >= k_max + 2 samples of the block's common window (full
          * position blocks only) at or below it, by binary search */
-        const int NBO = (int)((n + 63) >> 6);
+        const int NBO = (int)((o1 - o0 + 63) >> 6);
         for (int B = tid; B < NBO; B += WM_T) {
-            const int64_t ib = (int64_t)B << 6, ie = min<int64_t>(n, ib + 64) - 1;
+            const int64_t ib = o0 + ((int64_t)B << 6), ie = min<int64_t>(o1, ib + 64) - 1;
             int64_t s0, e0, s1, e1;
             win_bounds(ib, n, W, s0, e0);
             win_bounds(ie, n, W, s1, e1);
@@ -318,10 +360,13 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         const int64_t off = (W - 1) / 2;
         for (int pb = tid; pb < NPB; pb += WM_T) {
             const int64_t a = t0 + ((int64_t)pb << 6);
-            const int64_t ilo = a - off > 0 ? a - off : 0;
+            int64_t ilo = a - off > 0 ? a - off : 0;
             int64_t ihi = min<int64_t>(n - 1, a + 63 + W - off);
             if (ihi >= n - 1 - off) ihi = n - 1;             /* windows clamped at n are all alike */
-            const int B0 = (int)(ilo >> 6), B1 = (int)(ihi >> 6), len = B1 - B0 + 1;
+            ilo = ilo > o0 ? ilo : o0;                       /* this workgroup's outputs only */
+            ihi = ihi < o1 - 1 ? ihi : o1 - 1;
+            if (ihi < ilo) { thr[pb] = 0; lthr[pb] = NB; continue; }   /* no window here reaches it */
+            const int B0 = (int)((ilo - o0) >> 6), B1 = (int)((ihi - o0) >> 6), len = B1 - B0 + 1;
             const int j = 31 - __clz(len);
             const uint8_t *st = bstar + (size_t)j * (WM_MMAX / 64 + 2);
             thr[pb] = max(st[B0], st[B1 - (1 << j) + 1]);
@@ -368,10 +413,10 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         kc = s_mk;
         STAMP(13);
         if (kc > WM_PMAX) {                                  /* too many kept: the unpruned variant */
-            if (tid == 0) full[f] = 1;
+            if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
             return;
         }
-        if (tid == 0) full[f] = 0;
+        if (tid == 0 && !chunked) full[f] = 0;
         for (int pb = wid; pb < NPB; pb += NWV) {
             const uint64_t mk = kmask[pb];
             if ((mk >> lane) & 1) kpos[kpre[pb] + __popcll(mk & lanemask_lt())] = (uint16_t)((pb << 6) + lane);
@@ -608,7 +653,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         return r;
     };
     int vfirst = INT_MAX, vlast = -1;
-    for (int64_t i = tid; i < n; i += WM_T) {
+    for (int64_t i = o0 + tid; i < o1; i += WM_T) {
         int64_t s, e;
         win_bounds(i, n, W, s, e);
         const int64_t lo = s > t0 ? s : t0;
@@ -657,6 +702,13 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
     __syncthreads();
     STAMP(6);
     STAMP_FLUSH(A.stamps);
+    if (chunked) {                                           /* bfill / ffill over all chunks: k_rollq_fill */
+        if (tid == 0 && s_last >= 0) {
+            atomicMin(&A.vfirst[f], s_first);
+            atomicMax(&A.vlast[f], s_last);
+        }
+        return;
+    }
     /* ---- .bfill().ffill() ---- */
     const int first = s_first, last = s_last;
     if (last < 0) {

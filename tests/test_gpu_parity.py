@@ -776,3 +776,39 @@ def test_quantile_kernel_paths(det):
         assert _same(r["troughs"], ot)
         assert _same(r["floor"], of)
         assert _same(r["peaks"], O.raw_peaks(env, of, d, params))
+
+
+@pytest.mark.gpu
+def test_chunked_wavelet_matrix_on_long_recordings(det):
+    """Long recordings (n > WM_MMAX) take the pruned wavelet matrix over chunks
+    of outputs (default); the sorted-union kernel (BPMX_OPT_ROLLQ_NOPRUNE
+    sends them there) and the oracle give the same floor bit for bit.  Cases:
+    a late first trough (whole NaN chunks), a ramp, ulp-level floors, a
+    recording whose every chunk holds > WM_TRMAX troughs (falls back), and a
+    batch mixing short and long recordings."""
+    from bpm_analysis_amd import _native as N
+    rng = np.random.default_rng(21)
+    params = dict(G.BASE_PARAMS)
+    d = O.derive(302, params)
+
+    def beat(n, period):
+        t = np.arange(n)
+        return np.maximum(0.0, np.sin(2 * np.pi * t / period)) ** 8
+
+    n = 96_000                                                   # 5.3 min at 302 Hz
+    envs = [
+        200 + 80 * np.sin(np.arange(n) / 700.0) + 300 * beat(n, 250) + rng.random(n),
+        10.0 + 0.01 * np.arange(n) + 3000 * beat(n, 300) + rng.random(n),
+        10.0 + np.spacing(10.0) * rng.integers(0, 5, n) + 300 * beat(n, 250),
+        np.abs(np.sin(np.arange(n) / 9.0)) * 100 + rng.random(n),  # > 512 troughs per chunk
+        np.concatenate([np.linspace(500.0, 100.0, 40_000), 100 + 300 * beat(n - 40_000, 250) + rng.random(n - 40_000)]),
+        300 * beat(12_000, 250) + rng.random(12_000) + 20,          # short, same batch
+    ]
+    a = det.run_env_host(envs, 302, params, N.STAGE_FLOOR)
+    b = det.run_env_host(envs, 302, params, N.STAGE_FLOOR, options=N.OPT_ROLLQ_NOPRUNE)
+    for env, ra, rb in zip(envs, a, b):
+        assert _same(ra["floor"], rb["floor"])
+        assert _same(ra["troughs"], rb["troughs"])
+        of, ot, _ = O.noise_floor(env, d, params)
+        assert _same(ra["floor"], of)
+        assert _same(ra["troughs"], ot)
