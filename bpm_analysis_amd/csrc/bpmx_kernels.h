@@ -222,6 +222,10 @@ struct DraftBoundArgs {
 constexpr int DB_T = 256;
 constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */
 constexpr int DB_LOCAL_M = 512;  /* more troughs than this: per-window ranking instead of the global order */
+struct DbSeg {                   /* a trough-curve segment [s, e) and one of its end values */
+    int32_t s, e;
+    double v;
+};
 
 struct FinalArgs {
     const double *draft;

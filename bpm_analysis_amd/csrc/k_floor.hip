@@ -666,12 +666,46 @@ __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
  *   U = min{ hi_j : sum(len_i : hi_i <= hi_j) >= k + 2 (k + 1) } -> s_(k+1) <= U
  * keep iff env[t] <= mult r: certain when env[t] <= mult L, certainly not
  * when env[t] > mult U (1 + 2^-50); anything else makes the recording exact. */
+
+/* One walk over the segments in value order: the first whose cumulative
+ * in-window length passes thr (> thr, or >= thr with GE) gives the bound.  A
+ * segment lies in the window [lo, hi) iff its overlap is positive; records are
+ * read DB_WALK at a time ahead of the (sequential) accumulation. */
+template <bool GE>
+__device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int64_t lo, int64_t hi, int64_t thr) {
+    constexpr int DB_WALK = 8;
+    int64_t c = 0;
+    for (int r = 0; r < m; r += DB_WALK) {
+        DbSeg g[DB_WALK];
+#pragma unroll
+        for (int u = 0; u < DB_WALK; ++u) g[u] = sg[r + u < m ? r + u : m - 1];
+#pragma unroll
+        for (int u = 0; u < DB_WALK; ++u) {
+            const int64_t a = lo > g[u].s ? lo : (int64_t)g[u].s;
+            const int64_t b = hi < g[u].e ? hi : (int64_t)g[u].e;
+            if (r + u < m && b > a) {
+                c += b - a;
+                if (GE ? c >= thr : c > thr) return g[u].v;
+            }
+        }
+    }
+    return __builtin_inf();
+}
+
 __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
     __shared__ int32_t s_tp[DB_TRMAX];
     __shared__ double s_tv[DB_TRMAX];
-    __shared__ int16_t s_olo[DB_TRMAX], s_ohi[DB_TRMAX];     /* segments by lower / upper end value */
+    /* segments by lower / upper end value: up to DB_LOCAL_M - 1 troughs as
+     * {start, end, end value} records, so a walk step is one independent LDS
+     * read; beyond (BPMX_OPT_DRAFT_GLOBAL_RANK only) as index lists */
+    __shared__ union {
+        int16_t ord[2][DB_TRMAX];
+        DbSeg seg[2][DB_LOCAL_M - 1];      /* - 1: four workgroups per CU's LDS */
+    } s_o;
+    int16_t *s_olo = s_o.ord[0], *s_ohi = s_o.ord[1];
+    DbSeg *s_slo = s_o.seg[0], *s_shi = s_o.seg[1];
     __shared__ int s_vf, s_vl, s_undecided;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int m = A.nraw[f];
@@ -754,19 +788,36 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     auto tv = [&](int j) -> double { return s_tv[j - base]; };
     auto seg_lo = [&](int j) -> double { return j + 1 < m ? fmin(tv(j), tv(j + 1)) : tv(j); };
     auto seg_hi = [&](int j) -> double { return j + 1 < m ? fmax(tv(j), tv(j + 1)) : tv(j); };
-    /* stable ranks by end value (ties by index): order lists for the walks.
-     * Long recordings skip them (O(m^2)) and rank each window's few segments
-     * in place instead (below). */
-    for (int j = tid; j < m && !local; j += DB_T) {
+    /* stable ranks by end value (ties by index) of the ranked segments: all
+     * of them, or (long recordings) the staged ones whose both ends are staged
+     * — every segment a chunk window touches.  Under DB_LOCAL_M of them they
+     * become records for the walks; more, the order lists (recording-wide,
+     * BPMX_OPT_DRAFT_GLOBAL_RANK) or, for long recordings, each window's few
+     * segments ranked in place (below).  Ranking a subset keeps the relative
+     * order of the segments in it, so the walks stop on the same segment. */
+    const int nr = local ? (base + ns == m ? ns : ns - 1) : m;
+    const bool recs = nr > 0 && nr < DB_LOCAL_M;
+    for (int jr = tid; jr < nr && (recs || !local); jr += DB_T) {
+        const int j = base + jr;
         const double a = seg_lo(j), b = seg_hi(j);
         int ra = 0, rb = 0;
-        for (int i = 0; i < m; ++i) {
-            const double ai = seg_lo(i), bi = seg_hi(i);
+        double vc = s_tv[0];                       /* tv(i), carried: one LDS read per segment */
+#pragma unroll 4
+        for (int i = base; i < base + nr; ++i) {
+            const double vn = i + 1 < m ? s_tv[i + 1 - base] : vc;
+            const double ai = fmin(vc, vn), bi = fmax(vc, vn);
             ra += (ai < a || (ai == a && i < j)) ? 1 : 0;
             rb += (bi < b || (bi == b && i < j)) ? 1 : 0;
+            vc = vn;
         }
-        s_olo[ra] = (int16_t)j;
-        s_ohi[rb] = (int16_t)j;
+        if (recs) {
+            const int32_t se = j + 1 < m ? (int32_t)tp(j + 1) : (int32_t)n;
+            s_slo[ra] = DbSeg{(int32_t)tp(j), se, a};
+            s_shi[rb] = DbSeg{(int32_t)tp(j), se, b};
+        } else {
+            s_olo[ra] = (int16_t)j;
+            s_ohi[rb] = (int16_t)j;
+        }
     }
     __syncthreads();
     auto seg_of = [&](int64_t x) -> int {           /* last trough <= x (x >= t0), among the staged */
@@ -794,7 +845,10 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         /* L: first lower end (ascending) whose in-window cumulative length exceeds k;
          * U: first upper end (ascending) whose cumulative reaches thr_u */
         double L = __builtin_inf(), U = __builtin_inf();
-        if (!local) {
+        if (recs) {
+            L = db_walk<false>(s_slo, nr, lo, hi, k);
+            U = db_walk<true>(s_shi, nr, lo, hi, thr_u);
+        } else if (!local) {
             int64_t c = 0;
             for (int r = 0; r < m; ++r) {
                 const int b = s_olo[r];
