@@ -981,6 +981,7 @@ __device__ __forceinline__ Cx2 shfl_down_cx2(const Cx2 &x, int d) {
     return Cx2{__shfl_down(x.a1, d), __shfl_down(x.b1, d), __shfl_down(x.a2, d), __shfl_down(x.b2, d)};
 }
 
+constexpr int NAT_CPF = 8;      /* tiles per lane held in registers by k_native_carry */
 __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f]) return;
@@ -1034,12 +1035,35 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
 
     /* forward tile carries: car[t][0..3] = S0_t; car[t][4..7] temporarily
      * holds b_t = R0_t + G0 S0_t for the backward scan (same lane, same run) */
+    /* runs of at most NAT_CPF tiles (recordings up to ~108 s at 302 Hz) keep
+     * their tile records in registers: every load issued before the compose,
+     * and b_t stays in registers for the backward scan instead of a round trip
+     * through car[t][4..7] */
+    const bool pf = CH <= NAT_CPF;                          /* wave-uniform */
+    V4 ag[NAT_CPF], ar[NAT_CPF], bbr[NAT_CPF];
     {
         Cx2 P = ID;
         V4 acc = Z4;
-        for (int64_t t = tb0; t < te0; ++t) {
-            acc = add4(cx2_mv(MT, acc), nat_ld4(agg + t * 8));
-            P = cx2_mul(MT, P);
+        if (pf) {
+#pragma unroll
+            for (int u = 0; u < NAT_CPF; ++u) {
+                if (tb0 + u < te0) {
+                    ag[u] = nat_ld4(agg + (tb0 + u) * 8);
+                    ar[u] = nat_ld4(agg + (tb0 + u) * 8 + 4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < NAT_CPF; ++u) {
+                if (tb0 + u < te0) {
+                    acc = add4(cx2_mv(MT, acc), ag[u]);
+                    P = cx2_mul(MT, P);
+                }
+            }
+        } else {
+            for (int64_t t = tb0; t < te0; ++t) {
+                acc = add4(cx2_mv(MT, acc), nat_ld4(agg + t * 8));
+                P = cx2_mul(MT, P);
+            }
         }
         /* inclusive Kogge-Stone over lanes: x_l <- x_l o x_(l-d) */
 #pragma unroll
@@ -1056,13 +1080,25 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         V4 ax = shfl_up_v(acc, 1);
         if (lane == 0) { Px = ID; ax = Z4; }
         V4 s = add4(cx2_mv(Px, S), ax);                     /* carry into this lane's run */
-        for (int64_t t = tb0; t < te0; ++t) {
-            const V4 inc = nat_ld4(agg + t * 8), r0 = nat_ld4(agg + t * 8 + 4);
-            const V4 bb = add4(r0, mv(G0, s));
-            double *cw = car + t * 8;
-            cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
-            cw[4] = bb.a; cw[5] = bb.b; cw[6] = bb.c; cw[7] = bb.d;
-            s = add4(cx2_mv(MT, s), inc);
+        if (pf) {
+#pragma unroll
+            for (int u = 0; u < NAT_CPF; ++u) {
+                if (tb0 + u < te0) {
+                    bbr[u] = add4(ar[u], mv(G0, s));
+                    double *cw = car + (tb0 + u) * 8;
+                    cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
+                    s = add4(cx2_mv(MT, s), ag[u]);
+                }
+            }
+        } else {
+            for (int64_t t = tb0; t < te0; ++t) {
+                const V4 inc = nat_ld4(agg + t * 8), r0 = nat_ld4(agg + t * 8 + 4);
+                const V4 bb = add4(r0, mv(G0, s));
+                double *cw = car + t * 8;
+                cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
+                cw[4] = bb.a; cw[5] = bb.b; cw[6] = bb.c; cw[7] = bb.d;
+                s = add4(cx2_mv(MT, s), inc);
+            }
         }
         /* S after the last full tile: the run holding tile Tf-1 */
         if (Tf > 0) {
@@ -1109,9 +1145,19 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     {
         Cx2 P = ID;
         V4 acc = Z4;
-        for (int64_t t = te0 - 1; t >= tb0; --t) {
-            acc = add4(cx2_mv(MT, acc), nat_ld4(car + t * 8 + 4));
-            P = cx2_mul(MT, P);
+        if (pf) {
+#pragma unroll
+            for (int u = NAT_CPF - 1; u >= 0; --u) {
+                if (tb0 + u < te0) {
+                    acc = add4(cx2_mv(MT, acc), bbr[u]);
+                    P = cx2_mul(MT, P);
+                }
+            }
+        } else {
+            for (int64_t t = te0 - 1; t >= tb0; --t) {
+                acc = add4(cx2_mv(MT, acc), nat_ld4(car + t * 8 + 4));
+                P = cx2_mul(MT, P);
+            }
         }
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
@@ -1127,11 +1173,22 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         V4 ax = shfl_down_v(acc, 1);
         if (lane == 63) { Px = ID; ax = Z4; }
         V4 qq = add4(cx2_mv(Px, q), ax);                    /* Qe entering this lane's last tile */
-        for (int64_t t = te0 - 1; t >= tb0; --t) {
-            double *cw = car + t * 8;
-            const V4 bb = nat_ld4(cw + 4);
-            cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
-            qq = add4(cx2_mv(MT, qq), bb);
+        if (pf) {
+#pragma unroll
+            for (int u = NAT_CPF - 1; u >= 0; --u) {
+                if (tb0 + u < te0) {
+                    double *cw = car + (tb0 + u) * 8;
+                    cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
+                    qq = add4(cx2_mv(MT, qq), bbr[u]);
+                }
+            }
+        } else {
+            for (int64_t t = te0 - 1; t >= tb0; --t) {
+                double *cw = car + t * 8;
+                const V4 bb = nat_ld4(cw + 4);
+                cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
+                qq = add4(cx2_mv(MT, qq), bb);
+            }
         }
     }
 }
