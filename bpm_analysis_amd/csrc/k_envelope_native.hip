@@ -1038,7 +1038,9 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     /* runs of at most NAT_CPF tiles (recordings up to ~108 s at 302 Hz) keep
      * their tile records in registers: every load issued before the compose,
      * and b_t stays in registers for the backward scan instead of a round trip
-     * through car[t][4..7] */
+     * through car[t][4..7].  Longer runs go in chunks of NAT_CPF tiles with
+     * the chunk's loads issued first (one memory latency per chunk, not per
+     * tile) */
     const bool pf = CH <= NAT_CPF;                          /* wave-uniform */
     V4 ag[NAT_CPF], ar[NAT_CPF], bbr[NAT_CPF];
     {
@@ -1059,10 +1061,19 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
                     P = cx2_mul(MT, P);
                 }
             }
-        } else {
-            for (int64_t t = tb0; t < te0; ++t) {
-                acc = add4(cx2_mv(MT, acc), nat_ld4(agg + t * 8));
-                P = cx2_mul(MT, P);
+        } else {                                            /* long runs: chunks of NAT_CPF, loads first */
+            for (int64_t c0 = tb0; c0 < te0; c0 += NAT_CPF) {
+                V4 g[NAT_CPF];
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u)
+                    if (c0 + u < te0) g[u] = nat_ld4(agg + (c0 + u) * 8);
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u) {
+                    if (c0 + u < te0) {
+                        acc = add4(cx2_mv(MT, acc), g[u]);
+                        P = cx2_mul(MT, P);
+                    }
+                }
             }
         }
         /* inclusive Kogge-Stone over lanes: x_l <- x_l o x_(l-d) */
@@ -1091,13 +1102,25 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
                 }
             }
         } else {
-            for (int64_t t = tb0; t < te0; ++t) {
-                const V4 inc = nat_ld4(agg + t * 8), r0 = nat_ld4(agg + t * 8 + 4);
-                const V4 bb = add4(r0, mv(G0, s));
-                double *cw = car + t * 8;
-                cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
-                cw[4] = bb.a; cw[5] = bb.b; cw[6] = bb.c; cw[7] = bb.d;
-                s = add4(cx2_mv(MT, s), inc);
+            for (int64_t c0 = tb0; c0 < te0; c0 += NAT_CPF) {
+                V4 inc[NAT_CPF], r0[NAT_CPF];
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u) {
+                    if (c0 + u < te0) {
+                        inc[u] = nat_ld4(agg + (c0 + u) * 8);
+                        r0[u] = nat_ld4(agg + (c0 + u) * 8 + 4);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u) {
+                    if (c0 + u < te0) {
+                        const V4 bb = add4(r0[u], mv(G0, s));
+                        double *cw = car + (c0 + u) * 8;
+                        cw[0] = s.a; cw[1] = s.b; cw[2] = s.c; cw[3] = s.d;
+                        cw[4] = bb.a; cw[5] = bb.b; cw[6] = bb.c; cw[7] = bb.d;
+                        s = add4(cx2_mv(MT, s), inc[u]);
+                    }
+                }
             }
         }
         /* S after the last full tile: the run holding tile Tf-1 */
@@ -1154,9 +1177,18 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
                 }
             }
         } else {
-            for (int64_t t = te0 - 1; t >= tb0; --t) {
-                acc = add4(cx2_mv(MT, acc), nat_ld4(car + t * 8 + 4));
-                P = cx2_mul(MT, P);
+            for (int64_t c1 = te0 - 1; c1 >= tb0; c1 -= NAT_CPF) {   /* tiles c1, c1 - 1, ... */
+                V4 g[NAT_CPF];
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u)
+                    if (c1 - u >= tb0) g[u] = nat_ld4(car + (c1 - u) * 8 + 4);
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u) {
+                    if (c1 - u >= tb0) {
+                        acc = add4(cx2_mv(MT, acc), g[u]);
+                        P = cx2_mul(MT, P);
+                    }
+                }
             }
         }
 #pragma unroll
@@ -1183,11 +1215,19 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
                 }
             }
         } else {
-            for (int64_t t = te0 - 1; t >= tb0; --t) {
-                double *cw = car + t * 8;
-                const V4 bb = nat_ld4(cw + 4);
-                cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
-                qq = add4(cx2_mv(MT, qq), bb);
+            for (int64_t c1 = te0 - 1; c1 >= tb0; c1 -= NAT_CPF) {
+                V4 g[NAT_CPF];
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u)                  /* the chunk's b_t, read before it is overwritten */
+                    if (c1 - u >= tb0) g[u] = nat_ld4(car + (c1 - u) * 8 + 4);
+#pragma unroll
+                for (int u = 0; u < NAT_CPF; ++u) {
+                    if (c1 - u >= tb0) {
+                        double *cw = car + (c1 - u) * 8;
+                        cw[4] = qq.a; cw[5] = qq.b; cw[6] = qq.c; cw[7] = qq.d;
+                        qq = add4(cx2_mv(MT, qq), g[u]);
+                    }
+                }
             }
         }
     }
