@@ -6,9 +6,16 @@ recordings per GPU, inputs resident in HBM.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One process per GPU; files are sharded (weak scaling: every rank processes its
-own 1024 recordings, no data-path collective).  After the timed steps the
-per-file peak counts are gathered to rank 0 over RCCL (the only collective).
-Rank 0 prints one JSON line.
+own 1024 recordings, no data-path collective).  After the timed steps every
+file's raw peaks, final beats and BPM curve go to rank 0 over RCCL (the only
+collective besides the max-time all_reduce).  Rank 0 prints one JSON line.
+
+`python bench.py --gpus N` without WORLD_SIZE in the environment starts the N
+ranks itself (a `torch.distributed.run` child process, before anything touches
+the GPU) and exits with its status; a rank whose WORLD_SIZE differs from
+--gpus refuses to run.  `--cpu-stub` (tests only) swaps the GPU detector for
+tests/bench_stub.py's oracle-backed double over gloo, so the multi-rank path
+runs on a CPU-only host; its line says so and is never a measurement.
 """
 from __future__ import annotations
 
@@ -26,9 +33,12 @@ sys.path.insert(0, REPO)
 
 METRIC = "audio-samples/sec (filter+envelope+peaks), 1024x60s@44.1kHz batch, 1 & 8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# flags both sides report: static / draft / NaN floor (BPMX_F_TOO_SHORT and
+# BPMX_F_BAD_WINDOW are library-side input checks, compared by the tests)
+FLOOR_FLAGS = 1 | 2 | 4
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -53,7 +63,73 @@ def parse():
                          "64 x U[10, 30] min 96 kHz stereo per GPU (512 over 8 GPUs), ragged, LPT over ranks")
     ap.add_argument("--parity-files", type=int, default=16,
                     help="N > 1: files per rank checked against the oracle (N = 1 checks every file)")
-    return ap.parse_args()
+    ap.add_argument("--c5-files", type=int, default=512,
+                    help="C5: recordings in the whole job (LPT over the ranks; BASELINE C5 is 512 over 8 GPUs)")
+    ap.add_argument("--c5-chunk-gb", type=float, default=48.0,
+                    help="C5: a rank's recordings run in HBM-resident chunks of at most this much PCM")
+    ap.add_argument("--c5-parity-files", type=int, default=2,
+                    help="C5: each rank's shortest recordings checked against the oracle")
+    ap.add_argument("--dropin-files", type=int, default=3,
+                    help="side measurement: per-file latency of the reference's call sequence through the "
+                         "drop-in on 60 s WAV files (0: skip)")
+    ap.add_argument("--undecided-mult", type=float, default=1.0,
+                    help="side measurement: the step with trough_rejection_multiplier set to this, which leaves "
+                         "many troughs inside the draft-floor bracket (decided by draft_point); 0: skip")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="TESTS ONLY: oracle-backed detector (tests/bench_stub.py) over gloo on CPU ranks")
+    a = ap.parse_args(argv)
+    if a.cpu_stub:          # the side measurements need device memory and streams
+        a.pcie_steps = a.contexts = a.exact_steps = a.dropin_files = 0
+        a.undecided_mult = 0.0
+    return a
+
+
+def launch_ranks(argv, n: int) -> int:
+    """`--gpus N` without a launcher: start N ranks as one torch.distributed.run
+    child (one process per GPU, rendezvous on 127.0.0.1) and return its exit
+    status.  Runs before anything initialises the GPU; never exec."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def setup_rank(args):
+    """(world, rank, local rank, detector, backend) of this process.  Refuses a
+    world size other than --gpus, so a line never claims GPUs it did not use."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report")
+    backend = "gloo" if args.cpu_stub else "nccl"
+    if args.cpu_stub:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from bench_stub import StubDetector as Detector
+    else:
+        from bpm_analysis_amd.engine import Detector
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local, Detector(local), backend
+
+
+def sync(det):
+    """Wait for the detector's device (no-op for the CPU stub)."""
+    if det.device.type == "cuda":
+        import torch
+        torch.cuda.synchronize(det.device)
 
 
 def algorithmic_bytes(mode: str, n_files: int, n_frames: int, nd: int, ds: int, channels: int = 1) -> dict:
@@ -190,7 +266,7 @@ def compare_outputs(gpu: list, cpu: list, exact_env: bool) -> dict:
         env_rel, floor_rel = max(env_rel, de), max(floor_rel, df)
         p_ok = np.array_equal(g["peaks"], o["peaks"])
         t_ok = np.array_equal(g["troughs"], o["troughs"])
-        f_ok = (int(g["flags"]) & 7) == int(o["flags"])
+        f_ok = (int(g["flags"]) & FLOOR_FLAGS) == (int(o["flags"]) & FLOOR_FLAGS)
         pe += p_ok
         te += t_ok
         fe += f_ok
@@ -245,129 +321,214 @@ def c5_lengths(n_files: int, fs: int = 96000, seed: int = 2025):
     return (rng.integers(600, 1801, size=n_files) * fs).astype(np.int64)
 
 
+def c5_chunks(lengths, mine, channels: int, budget_bytes: int):
+    """A rank's recordings (longest first) cut into HBM-resident chunks of at
+    most `budget_bytes` of int16 PCM (at least one recording each)."""
+    chunks, cur, acc = [], [], 0
+    for i in mine:
+        b = int(lengths[i]) * channels * 2
+        if cur and acc + b > budget_bytes:
+            chunks.append(cur)
+            cur, acc = [], 0
+        cur.append(int(i))
+        acc += b
+    if cur:
+        chunks.append(cur)
+    return chunks
+
+
 def run_c5(args):
-    """Side workload (never the driver's headline): BASELINE config C5, 64
-    ragged 10-30 min 96 kHz stereo recordings per GPU (512 on 8 GPUs),
-    native mode.  Recordings are placed over ranks by shard.lpt_partition of
-    the frame counts (every rank derives the same placement), each rank
-    synthesises its own in HBM (seed = global recording index) and runs them
-    longest first in one ragged batch.  Prints one JSON line."""
+    """Side workload (never the driver's headline): BASELINE config C5, 512
+    ragged 10-30 min 96 kHz stereo int16 recordings in the whole job (strong
+    scaling: `--c5-files` is fixed whatever N), native mode.  Recordings are
+    placed over ranks by shard.lpt_partition of the frame counts (every rank
+    derives the same placement) and each rank synthesises its own in HBM (seed
+    = global recording index).  A rank runs its recordings longest first in
+    chunks of at most `--c5-chunk-gb` of PCM (512 recordings are ~236 GB, the
+    whole of one GPU's HBM at N = 1); each chunk is resident before its timed
+    steps, and a step is one pass over every chunk.  Chunk rounds are
+    bracketed by barriers, so the step time is the slowest rank's.  Prints one
+    JSON line."""
     import torch
     import torch.distributed as dist
 
     from bpm_analysis_amd import DEFAULT_PARAMS
     from bpm_analysis_amd.design import design
-    from bpm_analysis_amd.engine import Detector
     from bpm_analysis_amd.shard import FileResult, gather_file_results, lpt_partition
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    det = Detector(local)
+    world, rank, local, det, backend = setup_rank(args)
     params = dict(DEFAULT_PARAMS, save_filtered_wav=False)
-    fs, ch, per = 96000, 2, 64
-    lengths = c5_lengths(per * world, fs)
+    fs, ch = 96000, 2
+    lengths = c5_lengths(args.c5_files, fs)
     mine = lpt_partition(lengths, world)[rank]
-    fo = np.concatenate([[0], np.cumsum(lengths[mine])]).astype(np.int64)
     d = design(fs, params, log=False)
-    pcm = det.synth(fo, fs, ch, seeds=[100_000 + i for i in mine])
-    out = det.alloc(fo, d.ds, d.sr)
-    frames = int(fo[-1])
-    nd_tot = int(out.doff[-1])
+    chunks = c5_chunks(lengths, mine, ch, int(args.c5_chunk_gb * 2 ** 30))
+    n_rounds = len(chunks)
+    if world > 1:                       # every rank takes part in every chunk round
+        t = torch.tensor([n_rounds], dtype=torch.int64, device=det.device if backend == "nccl" else None)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_rounds = int(t.item())
+    pick = set(sorted(mine, key=lambda i: lengths[i])[:max(0, args.c5_parity_files)]) if not args.no_cpu else set()
+    kept, rows, kprof = {}, [], {}
+    frames = nd_tot = 0
+    elapsed = 0.0
+    for ci in range(n_rounds):
+        idx = chunks[ci] if ci < len(chunks) else []
+        step = None
+        if idx:
+            fo = np.concatenate([[0], np.cumsum(lengths[idx])]).astype(np.int64)
+            pcm = det.synth(fo, fs, ch, seeds=[100_000 + i for i in idx])
+            out = det.alloc(fo, d.ds, d.sr)
+            frames += int(fo[-1])
+            nd_tot += int(out.doff[-1])
 
-    def step():
-        det.run(pcm, fo, fs, params, mode="native", channels=ch, out=out, d=d, options=args.options)
+            def step():
+                det.run(pcm, fo, fs, params, mode="native", channels=ch, out=out, d=d, options=args.options)
 
-    abytes = algorithmic_bytes_total("native", len(mine), frames, nd_tot, ch)
-    det.profile(True)
-    for _ in range(max(1, args.warmup)):
-        step()
-    torch.cuda.synchronize()
-    det.profile(False)
-    kprof = det.profile_read()
+            det.profile(True)
+            for _ in range(max(1, args.warmup)):
+                step()
+            sync(det)
+            det.profile(False)
+            for k, (c, t) in det.profile_read().items():
+                c0, t0 = kprof.get(k, (0, 0.0))
+                kprof[k] = (c0 + c, t0 + t)
+        if world > 1:
+            dist.barrier()
+        sync(det)
+        t0 = time.perf_counter()
+        if step is not None:
+            for _ in range(args.steps):
+                step()
+        sync(det)
+        if world > 1:
+            dist.barrier()
+        elapsed += time.perf_counter() - t0
+        if idx:
+            host = out.to_host()
+            for k, i in enumerate(idx):
+                rows.append(FileResult(i, raw_peaks=host[k]["peaks"], flags=host[k]["flags"]))
+                if i in pick:
+                    kept[i] = {kk: (v.copy() if isinstance(v, np.ndarray) else v) for kk, v in host[k].items()}
+            del host, out, pcm
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    host = out.to_host()
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=det.device)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=det.device if backend == "nccl" else None)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    # parity: this rank's two shortest recordings against the oracle (bounded CPU time)
+    # parity: this rank's shortest recordings against the oracle (bounded CPU time)
     parity = None
-    if not args.no_cpu:
+    if pick:
         from oracle import oracle as O
-        pick = sorted(range(len(mine)), key=lambda k: lengths[mine[k]])[:2]
-        outs = []
-        for k in pick:
-            o = O.detect(O.synth(100_000 + mine[k], int(lengths[mine[k]]), fs, ch), fs, params, mode="native")
-            outs.append({kk: o[kk] for kk in ("env", "floor", "troughs", "peaks", "flags")})
-        parity = compare_outputs([host[k] for k in pick], outs, exact_env=False)
-        parity["files_checked"] = [int(mine[k]) for k in pick]
-    rows = [FileResult(int(i), raw_peaks=host[k]["peaks"], flags=host[k]["flags"]) for k, i in enumerate(mine)]
-    allres = gather_file_results(rows, len(lengths), device=det.device if world > 1 else None)
+        order = sorted(pick)
+
+        def one(i):
+            o = O.detect(O.synth(100_000 + i, int(lengths[i]), fs, ch), fs, params, mode="native")
+            return {kk: o[kk] for kk in ("env", "floor", "troughs", "peaks", "flags")}
+
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max(1, min(len(order), cpu_threads()[0]))) as ex:
+            outs = list(ex.map(one, order))
+        parity = compare_outputs([kept[i] for i in order], outs, exact_env=False)
+        parity["files_checked_rank0"] = order
+        if world > 1:
+            cnt = torch.tensor([parity["files"], parity["peaks_equal"], parity["troughs_equal"],
+                                parity["flags_equal"], 0 if parity["ok"] else 1], dtype=torch.float64,
+                               device=det.device if backend == "nccl" else None)
+            dist.all_reduce(cnt)
+            c = [int(x) for x in cnt.tolist()]
+            parity.update(files=c[0], peaks_equal=c[1], troughs_equal=c[2], flags_equal=c[3],
+                          ok=c[4] == 0, ranks=world)
+    allres = gather_file_results(rows, len(lengths), device=det.device if (world > 1 and backend == "nccl") else None)
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         total = int(lengths.sum()) * ch
-        kernels = {k: {"launches": c, "avg_ms": round(t / c, 4), "share": round(t / max(1, args.warmup) / ms, 4)}
+        wsteps = max(1, args.warmup)
+        kernels = {k: {"launches": c, "avg_ms": round(t / c, 4), "share": round(t / wsteps / ms, 4)}
                    for k, (c, t) in sorted(kprof.items())}
         roof = None
         if "k_native_blocks" in kprof:
             c, t = kprof["k_native_blocks"]
-            kms = t / max(1, args.warmup)
-            ach = abytes["k_native_blocks"] / (kms / 1e3) / 1e9
+            kms = t / wsteps
+            ach = frames * ch * 2 / (kms / 1e3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": "k_native_blocks",
-                    "kernel_ms_per_step": round(kms, 4), "algorithmic_bytes_per_step": abytes["k_native_blocks"]}
-        step_bytes = frames * ch * 2
+                    "kernel_ms_per_step_rank0": round(kms, 4), "algorithmic_bytes_per_step_rank0": frames * ch * 2}
+        step_bytes = total * 2
         line = {"metric": "audio-samples/sec (filter+envelope+peaks), C5: 512 x 10-30 min 96 kHz stereo over 8 GPUs",
                 "value": total / (elapsed / args.steps), "unit": "audio-samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-                "config": {"workload": f"C5 shard: {per} x U[10,30] min 96000 Hz stereo int16 per GPU "
-                                       f"({per * world} recordings, LPT over {world} ranks), native mode",
-                           "recordings_rank0": len(mine), "frames_rank0": frames,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": "cpu-stub (tests only; not a measurement)" if args.cpu_stub else "synthetic",
+                "config": {"workload": f"C5: {len(lengths)} x U[10,30] min 96000 Hz stereo int16 recordings in the "
+                                       f"job, LPT over {world} ranks, HBM-resident chunks of <= "
+                                       f"{args.c5_chunk_gb:g} GiB PCM, native mode",
+                           "recordings_rank0": len(mine), "chunks_rank0": len(chunks), "frames_rank0": frames,
                            "decimated_rank0": nd_tot, "parallelism": f"file-sharded x{world}"},
                 "roofline": roof,
                 "pipeline": {"hbm_bytes_per_step": step_bytes,
                              "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
-                             "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)},
-                "parity": parity, "kernels": kernels,
+                             "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / (HBM_PEAK_GBS * world), 5)},
+                "parity": parity, "kernels_rank0": kernels,
                 "result_gather": {"files": sum(1 for r in allres if r is not None),
-                                  "peaks": int(sum(len(r["raw_peaks"]) for r in allres if r is not None))}}
-        print(json.dumps(line))
+                                  "peaks": int(sum(len(r["raw_peaks"]) for r in allres
+                                                   if r is not None and "raw_peaks" in r))}}
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
+def dropin_latency(device: int, n_files: int, fs: int, secs: float, params: dict, mode: str) -> dict:
+    """Per-file latency of the reference's own call sequence for one WAV
+    (`analyze_wav_file`, bpm_analysis.py:1731-1740): preprocess_audio ->
+    _calculate_dynamic_noise_floor -> PeakClassifier._find_raw_peaks twice
+    (preliminary pass :1635 and main pass :1740, both via :89), through the
+    drop-in (dropin.py) on 60 s int16 WAVs written to a temporary directory.
+    Side measurement beside BASELINE's 28.9 ms/file (reference, one core, the
+    first three calls); the beat stages in between are not timed here."""
+    import tempfile
+
+    import torch
+    from scipy.io import wavfile
+
+    from bpm_analysis_amd import dropin
+    from bpm_analysis_amd.engine import default_detector
+    det = default_detector(device)
+    n = int(round(secs * fs))
+    p = dict(params, save_filtered_wav=False, bpmx_mode=mode)
+    times = []
+    with tempfile.TemporaryDirectory() as tmp:
+        paths = []
+        for f in range(n_files + 1):              # file 0 warms up the path (plans, scratch)
+            fo = np.array([0, n], dtype=np.int64)
+            pcm = det.synth(fo, fs, 1, seed0=50_000 + f).cpu().numpy()
+            path = os.path.join(tmp, f"dropin_{f}.wav")
+            wavfile.write(path, fs, pcm)
+            paths.append(path)
+        torch.cuda.synchronize(det.device)
+        for k, path in enumerate(paths):
+            t0 = time.perf_counter()
+            env, sr = dropin.preprocess_audio(path, p, tmp)
+            floor, troughs = dropin._calculate_dynamic_noise_floor(env, sr, p)
+            pk1 = dropin.find_raw_peaks(env, sr, p, floor.values)
+            pk2 = dropin.find_raw_peaks(env, sr, p, floor.values)
+            dt = time.perf_counter() - t0
+            if k > 0:
+                times.append(dt)
+            assert np.array_equal(pk1, pk2)
+    return {"mode": mode, "files": n_files, "ms_per_file": round(float(np.median(times)) * 1e3, 3),
+            "ms_min": round(min(times) * 1e3, 3), "calls": "preprocess_audio + _calculate_dynamic_noise_floor "
+            "+ 2 x _find_raw_peaks (WAV read included)", "reference_ms_per_file_1core": 28.9}
+
+
+def main(args):
     import torch
     import torch.distributed as dist
 
     from bpm_analysis_amd import DEFAULT_PARAMS
     from bpm_analysis_amd.design import design
-    from bpm_analysis_amd.engine import Detector
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    det = Detector(local)
+    world, rank, local, det, backend = setup_rank(args)
+    cdev = det.device if backend == "nccl" else None          # collectives' tensors: the GPU under RCCL
     params = dict(DEFAULT_PARAMS)
     params["save_filtered_wav"] = False
     fs, F = args.fs, args.files
@@ -386,7 +547,7 @@ def main():
     det.profile(True)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync(det)
     det.profile(False)
     wprof = {k: v for k, v in det.profile_read().items() if k in abytes}
     dom = max(wprof, key=lambda k: wprof[k][1]) if wprof else ""
@@ -396,11 +557,11 @@ def main():
     # step time carries no per-launch event overhead
     det.profile_only(dom)
     det.profile(True)
-    torch.cuda.synchronize()
+    sync(det)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync(det)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -414,7 +575,7 @@ def main():
     kprof_steps = max(3, min(args.steps, 10))
     for _ in range(kprof_steps):
         step()
-    torch.cuda.synchronize()
+    sync(det)
     det.profile(False)
     kprof = det.profile_read()
 
@@ -424,7 +585,6 @@ def main():
     pcie = None
     if args.pcie_steps > 0:
         host = pcm.cpu().pin_memory()
-        stream = torch.cuda.current_stream(det.device)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         for _ in range(args.pcie_steps):
@@ -434,13 +594,15 @@ def main():
         dt = (time.perf_counter() - t2) / args.pcie_steps
         pcie = {"value": F * n / dt, "unit": "audio-samples/s", "ms_per_step": dt * 1e3,
                 "h2d_bytes_per_step": F * n * 2, "steps": args.pcie_steps, "per_gpu": True}
-        del host, stream
+        del host
 
     # Side measurement (never `value`): the same batch as K sub-batches on K
     # library contexts and K streams, so the latency-bound per-recording
-    # kernels of one sub-batch fill the tails of another's.
+    # kernels of one sub-batch fill the tails of another's.  Outputs are
+    # compared with the timed batch's file by file, array by array.
     multi = None
     if args.contexts > 1 and F % args.contexts == 0:
+        from bpm_analysis_amd.engine import Detector
         K, per = args.contexts, F // args.contexts
         dets = [det] + [Detector(local) for _ in range(K - 1)]
         streams = [torch.cuda.Stream(det.device) for _ in range(K)]
@@ -462,19 +624,22 @@ def main():
             mstep()
         torch.cuda.synchronize()
         mdt = (time.perf_counter() - tm0) / msteps
+        mhost = [r for o in outs for r in o.to_host()]
+        same = all(np.array_equal(a[k], b[k], equal_nan=(k in ("env", "floor")))
+                   for a, b in zip(mhost, gpu_host) for k in ("env", "floor", "troughs", "peaks")) and \
+            all(a["flags"] == b["flags"] for a, b in zip(mhost, gpu_host))
         multi = {"contexts": K, "value": F * n / mdt, "unit": "audio-samples/s", "ms_per_step": mdt * 1e3,
-                 "steps": msteps, "per_gpu": True,
-                 "peaks_match": int(sum(int(o.n_peaks.sum()) for o in outs)) == int(out.n_peaks.sum())}
+                 "steps": msteps, "per_gpu": True, "outputs_identical": bool(same),
+                 "compared": "env, floor, troughs, peaks, flags of every file vs the timed batch"}
         for x in dets[1:]:
             x.close()
-        del outs, views, streams
+        del outs, views, streams, mhost
 
     # Side measurement (never `value`): the same step with the two exact but
     # input-dependent shortcuts off (draft-floor bracket, final-floor pruning),
     # i.e. the step a recording that defeats them costs.  Outputs must not change.
     exact = None
     if args.exact_steps > 0:
-        import torch as _t
         ref = [x.clone() for x in (out.floor, out.troughs, out.peaks, out.n_troughs, out.n_peaks, out.flags)]
         opt = args.options | 8 | 16       # BPMX_OPT_DRAFT_FULL | BPMX_OPT_ROLLQ_NOPRUNE
         det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=opt)
@@ -484,25 +649,68 @@ def main():
             det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=opt)
         torch.cuda.synchronize()
         edt = (time.perf_counter() - te0) / args.exact_steps
-        same = all(_t.equal(a, b) if a.dtype != _t.float64 else _t.equal(a.nan_to_num(-1.0), b.nan_to_num(-1.0))
+        same = all(torch.equal(a, b) if a.dtype != torch.float64 else
+                   torch.equal(a.nan_to_num(-1.0), b.nan_to_num(-1.0))
                    for a, b in zip(ref, (out.floor, out.troughs, out.peaks, out.n_troughs, out.n_peaks, out.flags)))
         exact = {"options": opt, "value": F * n / edt, "unit": "audio-samples/s", "ms_per_step": edt * 1e3,
                  "steps": args.exact_steps, "per_gpu": True, "outputs_identical": bool(same)}
         del ref
 
+    # Side measurement (never `value`): a batch whose troughs the draft-floor
+    # bracket does not decide (the synthetic generator leaves none open; real
+    # recordings such as the vulpine sample leave ~17 %).  Lowering
+    # trough_rejection_multiplier puts many troughs near the threshold; they are
+    # then decided from the exact draft value at the trough (draft_point).  The
+    # same parameters with the draft computed in full must give identical outputs.
+    undecided = None
+    if args.undecided_mult > 0 and args.exact_steps > 0:
+        from bpm_analysis_amd import _native as N
+        pu = dict(params, trough_rejection_multiplier=args.undecided_mult)
+        det.run(pcm, fo, fs, pu, mode=args.mode, out=out, d=d, options=args.options | N.OPT_STATS)
+        stt = det.stats()
+        res = {}
+        for name, opt in (("default", args.options), ("draft_full", args.options | N.OPT_DRAFT_FULL),
+                          ("draft_full_noprune", args.options | N.OPT_DRAFT_FULL | N.OPT_ROLLQ_NOPRUNE)):
+            det.run(pcm, fo, fs, pu, mode=args.mode, out=out, d=d, options=opt)
+            torch.cuda.synchronize()
+            tu0 = time.perf_counter()
+            for _ in range(args.exact_steps):
+                det.run(pcm, fo, fs, pu, mode=args.mode, out=out, d=d, options=opt)
+            torch.cuda.synchronize()
+            res[name] = {"options": opt, "ms_per_step": (time.perf_counter() - tu0) / args.exact_steps * 1e3,
+                         "outputs": [x.clone() for x in (out.floor, out.troughs, out.peaks, out.n_troughs,
+                                                         out.n_peaks, out.flags)]}
+        base = res["default"]["outputs"]
+        for name in res:
+            o = res[name].pop("outputs")
+            res[name]["outputs_identical_to_default"] = bool(all(
+                torch.equal(a.nan_to_num(-1.0), b.nan_to_num(-1.0)) if a.dtype == torch.float64 else torch.equal(a, b)
+                for a, b in zip(base, o)))
+        undecided = {"trough_rejection_multiplier": args.undecided_mult, "raw_troughs": stt["raw_troughs"],
+                     "undecided_troughs": stt["undecided"],
+                     "undecided_frac": stt["undecided"] / max(1, stt["raw_troughs"]),
+                     "full_draft_chunks": stt["full_draft_chunks"], "steps": args.exact_steps, "per_gpu": True,
+                     **res}
+        del base
+
     # Parity of the timed batch against the oracle on the same recordings.  N = 1:
     # every file, in the cpu_baseline leg below.  N > 1: a bounded sample of
-    # every rank's shard, counts summed over ranks.
-    parity = None
+    # every rank's shard, counts summed over ranks; rank 0's sample, timed on
+    # its share of the host's cores, is that rank's cpu_baseline.
+    parity = cpu = None
     if world > 1 and args.parity_files > 0 and not args.no_cpu:
         lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-        th = max(1, cpu_threads()[0] // max(1, lw))
+        th_all, aff, ncpu = cpu_threads()
+        # OMP_NUM_THREADS, when set, is already this process's share (the launcher
+        # passes it to every rank); otherwise split the affinity mask over the ranks
+        th = th_all if os.environ.get("OMP_NUM_THREADS", "").isdigit() else max(1, th_all // max(1, lw))
         pick = sorted(set(np.linspace(0, F - 1, min(F, args.parity_files)).astype(int).tolist()))
-        outs, _ = oracle_outputs(args.mode, fs, n, [shard_seed0(rank, F) + f for f in pick], params, th)
+        seeds = [shard_seed0(rank, F) + f for f in pick]
+        outs, odt = oracle_outputs(args.mode, fs, n, seeds, params, th)
         pr = compare_outputs([gpu_host[f] for f in pick], outs, exact_env=(args.mode == "reference"))
         cnt = torch.tensor([pr["files"], pr["peaks_equal"], pr["troughs_equal"], pr["flags_equal"]],
-                           dtype=torch.float64, device=det.device)
-        worst = torch.tensor([pr["env_max_rel"], pr["floor_max_rel"]], dtype=torch.float64, device=det.device)
+                           dtype=torch.float64, device=cdev)
+        worst = torch.tensor([pr["env_max_rel"], pr["floor_max_rel"]], dtype=torch.float64, device=cdev)
         dist.all_reduce(cnt)
         dist.all_reduce(worst, op=dist.ReduceOp.MAX)
         c, w = cnt.tolist(), worst.tolist()
@@ -510,6 +718,14 @@ def main():
                   "troughs_equal": int(c[2]), "flags_equal": int(c[3]), "env_max_rel": w[0], "floor_max_rel": w[1],
                   "env_tol": pr["env_tol"],
                   "ok": c[1] == c[0] and c[2] == c[0] and c[3] == c[0] and max(w) <= pr["env_tol"]}
+        if rank == 0:
+            cpu = {"value": len(pick) * n / odt, "unit": "audio-samples/s", "cores": th, "kind": "port",
+                   "per_rank": True, "rank": 0, "affinity_cpus": aff, "os_cpu_count": ncpu,
+                   "sample": f"rank 0's parity sample: {len(pick)} of its {F} recordings (seeds {seeds[0]}.."
+                             f"{seeds[-1]}, {n / fs:.0f} s {fs} Hz mono int16), {args.mode} mode, "
+                             f"oracle/bpmx_oracle.c + numpy FFT on {th} threads of {_cpu_model()} ({lw} ranks "
+                             f"on this node, each on its share), while the other ranks ran theirs; "
+                             f"{odt:.2f} s wall"}
 
     # Side measurement (never `value`): the host beat stages (beats.py: classifier,
     # refinement, BPM curve, metrics — SURVEY 8(f) rows 1 and 3) on the first
@@ -547,7 +763,7 @@ def main():
                                  "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))},
                       "native_equals_python": bool(same)}
     tg0 = time.perf_counter()
-    allres = gather_file_results(rows, world * F, device=det.device if world > 1 else None)
+    allres = gather_file_results(rows, world * F, device=cdev if world > 1 else None)
     gathered = None
     if rank == 0:
         got = [r for r in allres if r is not None]
@@ -555,7 +771,15 @@ def main():
                     "bpm_curves": int(sum(1 for r in got if len(r["bpm"]))),
                     "bpm_points": int(sum(len(r["bpm"]) for r in got)),
                     "final_beats": int(sum(len(r["final_peaks"]) for r in got)),
+                    "ranks_seen": sorted({int(r["rank"]) for r in got}),
                     "ms": round((time.perf_counter() - tg0) * 1e3, 2)}
+
+    # Side measurement (never `value`): one recording at a time through the
+    # drop-in, as the reference's analyze_wav_file calls it (rank 0 only).
+    dropin = None
+    if rank == 0 and args.dropin_files > 0:
+        dropin = {m: dropin_latency(local, args.dropin_files, fs, args.secs, params, m)
+                  for m in ("reference", "native")}
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -588,16 +812,17 @@ def main():
                     kernels[k]["pmc_bytes_per_step"] = tr
         # whole-step view of the north-star roofline: PCM bytes (read once) / step time
         step_bytes = F * n * 2
-        pipeline = {"hbm_bytes_per_step": step_bytes, "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
+        pipeline = {"hbm_bytes_per_step": step_bytes, "per_gpu": True,
+                    "achieved_GBps": round(step_bytes / (ms / 1e3) / 1e9, 1),
                     "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
-        cpu = None
         if world == 1 and not args.no_cpu and args.cpu_files != 0:
             nfc = args.cpu_files if args.cpu_files > 0 else F
             cpu, parity = cpu_baseline(args.mode, fs, n, shard_seed0(rank, F), nfc, params, gpu_host)
         line = {
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "cpu-stub (tests only; not a measurement)" if args.cpu_stub else "synthetic",
             "config": {"workload": workload,
                        "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
                        "parallelism": f"file-sharded x{world}"},
@@ -605,15 +830,22 @@ def main():
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
             "result_gather": gathered, "multi_context": multi, "exact_no_shortcuts": exact,
-            "host_beat_stages": host_beats,
+            "host_beat_stages": host_beats, "dropin_latency": dropin, "draft_undecided": undecided,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    if parse().workload == "c5":
-        run_c5(parse())
+    _args = parse()
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if not _args.cpu_stub:
+            import torch
+            if torch.cuda.device_count() < _args.gpus:      # counts devices without initialising them
+                raise SystemExit(f"bench.py: --gpus {_args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(launch_ranks(sys.argv[1:], _args.gpus))
+    if _args.workload == "c5":
+        run_c5(_args)
     else:
-        main()
+        main(_args)

@@ -31,10 +31,13 @@ OPT_NATIVE_DMA = 128
 OPT_PEAKS_GLOBAL = 256
 OPT_HILBERT_R2C = 512
 OPT_REF_SERIAL_MEAN = 1024
+OPT_STATS = 2048
+STAT_RAW_TROUGHS, STAT_UNDECIDED, STAT_FULL_DRAFT, NSTATS = 0, 1, 2, 8
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",
-           "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only"]
+           "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only",
+           "bpmx_stats"]
 
 
 class Params(ctypes.Structure):
@@ -61,7 +64,18 @@ class Out(ctypes.Structure):
 
 
 class BpmxError(RuntimeError):
-    pass
+    """A libbpmx failure.  ``code`` is the BPMX_E_* status (None when raised by
+    the host side).  Only argument and size-limit errors belong to the
+    recordings of one call (``per_file``); a HIP or device failure means the
+    GPU path itself failed and must stop the run."""
+
+    def __init__(self, msg: str = "", code: int = None):
+        super().__init__(msg)
+        self.code = code
+
+    @property
+    def per_file(self) -> bool:
+        return self.code in (E_ARG, E_LIMIT)
 
 
 class BpmxArgError(BpmxError, ValueError):
@@ -103,6 +117,8 @@ def load() -> ctypes.CDLL:
     L.bpmx_profile_read.restype = ctypes.c_int
     L.bpmx_profile_only.argtypes = [P, ctypes.c_char_p]
     L.bpmx_profile_only.restype = ctypes.c_int
+    L.bpmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    L.bpmx_stats.restype = ctypes.c_int
     if L.bpmx_abi_version() != ABI_VERSION:
         raise BpmxError(f"libbpmx ABI {L.bpmx_abi_version()} != expected {ABI_VERSION}; rebuild")
     _lib = L
@@ -113,5 +129,5 @@ def check(rc: int, what: str) -> None:
     if rc != OK:
         msg = load().bpmx_last_error().decode(errors="replace")
         if rc == E_ARG:
-            raise BpmxArgError(msg)
-        raise BpmxError(f"{what} failed ({rc}): {msg}")
+            raise BpmxArgError(msg, rc)
+        raise BpmxError(f"{what} failed ({rc}): {msg}", rc)

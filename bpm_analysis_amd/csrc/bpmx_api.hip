@@ -226,6 +226,19 @@ int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len) {
     return (int)s.size();
 }
 
+int bpmx_stats(bpmx_ctx *ctx, int64_t *out, int n) {
+    if (!ctx || !out || n < 0) return fail(BPMX_E_ARG, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int64_t h[BPMX_NSTATS] = {};
+    auto it = ctx->bufs.find("stats");
+    if (it != ctx->bufs.end()) {
+        HIP_TRY(hipStreamSynchronize(ctx->stats_stream));
+        HIP_TRY(hipMemcpy(h, it->second.first, sizeof h, hipMemcpyDeviceToHost));
+    }
+    for (int i = 0; i < n; ++i) out[i] = i < BPMX_NSTATS ? h[i] : 0;
+    return BPMX_NSTATS;
+}
+
 int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {
     if (!ctx || !P || !B || !O) return fail(BPMX_E_ARG, "NULL argument");
     const int F = B->n_files;
@@ -250,6 +263,14 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     if (do_env && P->env_window < 1) return fail(BPMX_E_ARG, "envelope window must be >= 1");
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
+    int64_t *d_stats = nullptr;
+    if (P->options & BPMX_OPT_STATS) {
+        int src = BPMX_OK;
+        d_stats = (int64_t *)ctx->buf("stats", BPMX_NSTATS * 8, &src);
+        if (src != BPMX_OK) return src;
+        HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
+        ctx->stats_stream = s;
+    }
 
     /* ---- geometry ---- */
     std::vector<int64_t> foff(F + 1), doff(F + 1), boff(F + 1);
@@ -623,6 +644,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
             a.dec = tdec; a.exact = d_exact;
             a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
+            a.stats = d_stats;
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
             const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);

@@ -39,6 +39,7 @@ struct bpmx_ctx {
     bool nat_tiles_dirty = false;
     bool nat_tab_dirty = false;
     bool prof = false;
+    hipStream_t stats_stream = nullptr;          /* stream of the last run with BPMX_OPT_STATS */
     struct Rec { std::string name; hipEvent_t a, b; };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;

@@ -215,9 +215,12 @@ struct DraftBoundArgs {
     const int32_t *run;      /* [F] files with >= 5 raw troughs */
     int32_t n_files, window, min_periods;
     double q, mult;
-    uint8_t *dec;            /* [doff + j]: 1 keep, 0 reject, 2 undecided */
-    int32_t *exact;          /* [F] out: 1 = needs the full draft (undecided trough, all-NaN draft, too many troughs) */
+    uint8_t *dec;            /* [doff + j]: 1 keep, 0 reject (2 while undecided, then resolved by draft_point) */
+    int32_t *exact;          /* [F] out: 1 = needs the full draft (all-NaN draft, too many troughs, a window
+                                draft_point does not take) */
     int32_t local_m;         /* more troughs than this: rank segments per window (DB_LOCAL_M) */
+    int64_t *stats;          /* optional (BPMX_OPT_STATS): += raw troughs, undecided troughs, chunks sent to the
+                                full draft by draft_point */
 };
 constexpr int DB_T = 256;
 constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */

@@ -13,6 +13,8 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
                     const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active);
 /* k_bluestein.hip: hb = N * Hilbert transform of yd for the listed recordings */
+/* rocfft_setup() exactly once per process (std::call_once), whatever thread gets there first */
+int rocfft_setup_once();
 int bluestein_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, const std::vector<int64_t> &doff,
                       const int64_t *d_doff, const std::vector<int32_t> &files);
 }

@@ -30,6 +30,7 @@
  *   k_blu_post   g_m = conj(c_m) conv_m / L -> h
  */
 #include <map>
+#include <mutex>
 #include <tuple>
 
 #include <rocfft/rocfft.h>
@@ -171,20 +172,19 @@ struct C2cPlans {
     rocfft_plan fwd = nullptr, bwd = nullptr;
     size_t work = 0;
 };
+/* process-wide (contexts on any thread share plans): lookups and inserts under
+ * g_c2c_mu; map nodes are never erased, so a returned pointer stays valid */
 std::map<std::tuple<int, int64_t, int64_t>, C2cPlans> g_c2c;   /* (device, L, batch) */
+std::mutex g_c2c_mu;
 
 int rf_fail(const char *what, rocfft_status st) {
     return fail(BPMX_E_HIP, std::string(what) + " failed (rocfft status " + std::to_string((int)st) + ")");
 }
 
 int c2c_plans(int dev, int64_t L, int64_t batch, C2cPlans **out) {
-    static bool setup = false;
-    if (!setup) {
-        const rocfft_status st = rocfft_setup();
-        if (st != rocfft_status_success) return rf_fail("rocfft_setup", st);
-        setup = true;
-    }
+    if (const int rc = rocfft_setup_once(); rc != BPMX_OK) return rc;
     const auto key = std::make_tuple(dev, L, batch);
+    std::lock_guard<std::mutex> g(g_c2c_mu);
     auto it = g_c2c.find(key);
     if (it != g_c2c.end()) { *out = &it->second; return BPMX_OK; }
     C2cPlans p;
@@ -254,7 +254,7 @@ int bluestein_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb
     int32_t *d_files = (int32_t *)ctx->buf("blu_files", hf.size() * 4, &rc);
     if (rc != BPMX_OK) return rc;
     const bool make_b = grew || key != ctx->blu_key;
-    ctx->blu_key = key;
+    ctx->blu_key.clear();                 /* set again only once every group's FFT(b) table is built */
     HIP_TRY(hipMemcpyAsync(d_files, hf.data(), hf.size() * 4, hipMemcpyHostToDevice, s));
     size_t off = 0, fo = 0;
     for (auto &g : groups) {
@@ -281,6 +281,7 @@ int bluestein_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb
         off += (size_t)L * nrec;
         fo += nrec;
     }
+    ctx->blu_key = key;
     return BPMX_OK;
 }
 

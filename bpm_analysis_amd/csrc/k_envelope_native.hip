@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <tuple>
 #include <vector>
 
@@ -1297,20 +1298,29 @@ struct FftPlans {
     rocfft_plan fwd = nullptr, inv = nullptr;
     size_t work = 0;
 };
+/* process-wide, shared by contexts on any thread: find/insert under g_plans_mu
+ * (nodes are never erased, so returned pointers stay valid) */
 std::map<std::tuple<int, int64_t, int64_t>, FftPlans> g_plans;   /* (device, nd, batch) */
-bool g_fft_setup = false;
+std::mutex g_plans_mu;
 
 int fft_fail(const char *what, rocfft_status st) {
     return fail(BPMX_E_HIP, std::string(what) + " failed (rocfft status " + std::to_string((int)st) + ")");
 }
 
+}  // namespace
+
+int rocfft_setup_once() {
+    static std::once_flag once;
+    static rocfft_status st = rocfft_status_success;
+    std::call_once(once, [] { st = rocfft_setup(); });
+    return st == rocfft_status_success ? BPMX_OK : fft_fail("rocfft_setup", st);
+}
+
+namespace {
 int get_plans(int dev, int64_t nd, int64_t batch, FftPlans **out) {
-    if (!g_fft_setup) {
-        rocfft_status st = rocfft_setup();
-        if (st != rocfft_status_success) return fft_fail("rocfft_setup", st);
-        g_fft_setup = true;
-    }
+    if (const int rc = rocfft_setup_once(); rc != BPMX_OK) return rc;
     auto key = std::make_tuple(dev, nd, batch);
+    std::lock_guard<std::mutex> g(g_plans_mu);
     auto it = g_plans.find(key);
     if (it != g_plans.end()) { *out = &it->second; return BPMX_OK; }
     FftPlans p;
@@ -1703,10 +1713,12 @@ struct HbTables {
     size_t lds = 0;
     double2 *dev = nullptr;
 };
-std::map<std::tuple<int, int64_t, int>, HbTables> g_hb;
+std::map<std::tuple<int, int64_t, int>, HbTables> g_hb;   /* under g_hb_mu, never erased */
+std::mutex g_hb_mu;
 
 HbTables *hb_tables(bpmx_ctx *ctx, int64_t nd, int window, HilbPlan *P, size_t *lds, hipStream_t s, int *rc) {
     const auto key = std::make_tuple(ctx->device, nd, window);
+    std::lock_guard<std::mutex> g(g_hb_mu);
     auto it = g_hb.find(key);
     if (it == g_hb.end()) {
         HbTables t;

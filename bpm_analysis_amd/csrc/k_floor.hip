@@ -692,6 +692,140 @@ __device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int64_t lo, in
     return __builtin_inf();
 }
 
+/* Exact draft value at one raw trough, by one wave (every lane active, wave-
+ * uniform arguments): the centred rolling quantile of the trough curve at
+ * output qp, i.e. k-th / (k+1)-th smallest of the window [lo, hi) of
+ * interp_at's values (bpm_analysis.py:1081-1086).  The window covers segments
+ * jl..jh of the staged troughs; lane l owns segments jl + l + 64 r.  Within a
+ * segment the values fl(slope (x - t_j)) + y_j are weakly monotone in x
+ * (rounding is monotone), so in ascending order they read val(a + i) on a
+ * rising segment and val(b - 1 - i) on a falling one, and the number below a
+ * value is one binary search.  Selection by random pivots: each round takes an
+ * active element uniformly (wave prefix scan), counts the elements < and <= it
+ * in every segment, and keeps the side holding rank k: expected O(log nobs)
+ * rounds.  The (k+1)-th is the k-th itself when enough equal it, else the least
+ * element above it (one more binary search position per segment).  Returns
+ * false for what it does not take (more than 64 DP_SPL segments, non-finite
+ * trough values): the recording then gets the full draft. */
+constexpr int DP_SPL = 4;
+
+__device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s_tv, int base, int m, int64_t n,
+                                            int64_t lo, int64_t hi, int jl, int jh, double q, uint32_t seed,
+                                            double *res) {
+    const int lane = lane_id();
+    if (jh - jl + 1 > 64 * DP_SPL) return false;
+    int32_t sa[DP_SPL], sn[DP_SPL], st[DP_SPL], slo[DP_SPL], shi[DP_SPL], sub[DP_SPL];
+    double sy[DP_SPL], ssl[DP_SPL];
+    bool sinc[DP_SPL], scst[DP_SPL];
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < DP_SPL; ++r) {
+        const int i = jl + lane + 64 * r;
+        sn[r] = 0; sa[r] = 0; st[r] = 0; sy[r] = 0.0; ssl[r] = 0.0; sinc[r] = true; scst[r] = true;
+        if (i <= jh) {
+            const int64_t tj = s_tp[i - base];
+            const int64_t nx = i + 1 < m ? (int64_t)s_tp[i + 1 - base] : n;
+            const int64_t a = lo > tj ? lo : tj, b = hi < nx ? hi : nx;
+            const double y0 = s_tv[i - base];
+            double y1 = y0, sl = 0.0;
+            if (i + 1 < m) {
+                y1 = s_tv[i + 1 - base];
+                sl = (y1 - y0) / ((double)nx - (double)tj);      /* interp_at's slope */
+                scst[r] = false;
+            }
+            ok = ok && __builtin_isfinite(y0) && __builtin_isfinite(y1) && __builtin_isfinite(sl);
+            sa[r] = (int32_t)a; sn[r] = (int32_t)(b - a); st[r] = (int32_t)tj;
+            sy[r] = y0; ssl[r] = sl; sinc[r] = y1 >= y0;
+        }
+        slo[r] = 0; shi[r] = sn[r]; sub[r] = 0;
+    }
+    if (__ballot(!ok) != 0) return false;
+    /* value of segment r at ascending rank i (interp_at, -ffp-contract=off) */
+    auto sorted = [&](int r, int i) -> double {
+        const int64_t x = sinc[r] ? (int64_t)sa[r] + i : (int64_t)sa[r] + sn[r] - 1 - i;
+        if (scst[r] || x == st[r]) return sy[r];
+        return ssl[r] * ((double)x - (double)st[r]) + sy[r];
+    };
+    const int64_t nobs = hi - lo;
+    double idxf = 0.0;
+    int64_t k = 0;
+    if (nobs > 1) {
+        idxf = q * (double)(nobs - 1);
+        k = (int64_t)idxf;
+    }
+    const bool interp = !(nobs == 1 || (double)k == idxf);
+    int64_t below = 0, leq = -1;
+    double va = 0.0;
+    uint32_t rng = seed;
+    for (int it = 0; it < 256; ++it) {
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < DP_SPL; ++r) cnt += shi[r] - slo[r];
+        const int incl = wave_iscan_dpp<false>(cnt);
+        const int tot = __shfl(incl, 63);
+        if (tot <= 0) return false;
+        rng = rng * 1664525u + 1013904223u;
+        const int p = (int)(((uint64_t)rng * (uint64_t)tot) >> 32);
+        const int excl = incl - cnt;
+        const bool own = p >= excl && p < incl;
+        const int owner = __ffsll((unsigned long long)__ballot(own)) - 1;
+        double pvl = 0.0;
+        if (own) {
+            int off = p - excl;
+#pragma unroll
+            for (int r = 0; r < DP_SPL; ++r) {
+                const int c = shi[r] - slo[r];
+                if (off >= 0 && off < c) pvl = sorted(r, slo[r] + off);
+                off -= c;
+            }
+        }
+        const double pv = __shfl(pvl, owner);
+        int slb[DP_SPL];
+        int cl = 0, ce = 0;
+#pragma unroll
+        for (int r = 0; r < DP_SPL; ++r) {
+            int l = slo[r], h = shi[r];
+            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) < pv) l = mid + 1; else h = mid; }
+            slb[r] = l;
+            h = shi[r];
+            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) <= pv) l = mid + 1; else h = mid; }
+            sub[r] = l;
+            cl += slb[r] - slo[r];
+            ce += sub[r] - slo[r];
+        }
+        const int64_t nless = below + wave_sum_i(cl), nleq = below + wave_sum_i(ce);
+        if (k < nless) {
+#pragma unroll
+            for (int r = 0; r < DP_SPL; ++r) shi[r] = slb[r];
+        } else if (k < nleq) {
+            va = pv;
+            leq = nleq;
+            break;
+        } else {
+            below = nleq;
+#pragma unroll
+            for (int r = 0; r < DP_SPL; ++r) slo[r] = sub[r];
+        }
+    }
+    if (leq < 0) return false;
+    if (!interp) {
+        *res = va;
+        return true;
+    }
+    double vb = va;
+    if (leq < k + 2) {
+        /* the least element above va: position sub in each segment (the cut
+         * above shi holds only larger values) */
+        double mn = __builtin_inf();
+#pragma unroll
+        for (int r = 0; r < DP_SPL; ++r)
+            if (sub[r] < sn[r]) mn = fmin(mn, sorted(r, sub[r]));
+        vb = wave_min(mn);
+    }
+    *res = va + (vb - va) * (idxf - (double)k);
+    return true;
+}
+
 __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
@@ -706,7 +840,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     } s_o;
     int16_t *s_olo = s_o.ord[0], *s_ohi = s_o.ord[1];
     DbSeg *s_slo = s_o.seg[0], *s_shi = s_o.seg[1];
-    __shared__ int s_vf, s_vl, s_undecided;
+    __shared__ int s_vf, s_vl, s_undecided, s_nund;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int m = A.nraw[f];
     const int tid = threadIdx.x;
@@ -726,7 +860,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int64_t *raw = A.raw + d0;
     const double *env = A.env + d0;
     const int64_t W = A.window, t0 = raw[0], off = (W - 1) / 2;
-    if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; }
+    if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; s_nund = 0; }
     __syncthreads();
     /* valid outputs (nobs >= min_periods) form one interval: with s >= t0 and
      * e <= n (outputs [t0 + W - 1 - off, n - 1 - off]) nobs = W >= min_periods,
@@ -891,7 +1025,35 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     }
     if (any_undecided) s_undecided = 1;
     __syncthreads();
-    if (tid == 0 && s_undecided) A.exact[f] = 1;         /* zeroed before the launch */
+    if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)(jc1 - jc0));
+    if (!s_undecided) return;
+    /* Undecided troughs: the exact draft value at each, one wave per trough
+     * (draft_point) over the staged troughs, which cover every window of the
+     * chunk.  The segment records are no longer read: their LDS holds the list. */
+    int16_t *s_und = s_o.ord[0];
+    for (int j = jc0 + tid; j < jc1; j += DB_T)
+        if (A.dec[d0 + j] == 2) s_und[atomicAdd(&s_nund, 1)] = (int16_t)(j - jc0);
+    __syncthreads();
+    const int nu = s_nund;
+    bool fail = false;
+    for (int u = wave_id(); u < nu; u += DB_T / 64) {
+        const int j = jc0 + s_und[u];
+        const int64_t t = tp(j);
+        const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
+        int64_t s, e;
+        win_bounds(qp, n, W, s, e);
+        const int64_t lo = s > t0 ? s : t0, hi = e;
+        double r = 0.0;
+        if (!draft_point(s_tp, s_tv, base, m, n, lo, hi, seg_of(lo), seg_of(hi - 1), A.q,
+                         0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu, &r)) {
+            fail = true;
+            continue;
+        }
+        if (lane_id() == 0) A.dec[d0 + j] = (r == r && tv(j) <= A.mult * r) ? 1 : 0;
+    }
+    if (fail && lane_id() == 0) A.exact[f] = 1;          /* zeroed before the launch */
+    if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
+    if (A.stats && fail && lane_id() == 0) atomicAdd((unsigned long long *)&A.stats[2], 1ull);
 }
 
 __global__ __launch_bounds__(256) void k_floor_final(FinalArgs A) {

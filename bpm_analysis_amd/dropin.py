@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 import warnings
 from typing import Dict, List, Sequence, Tuple
 
@@ -62,13 +63,52 @@ def _write_debug_wav(path: str, sr: int, y: np.ndarray) -> None:
         wavfile.write(path, sr, np.int16(y / np.max(np.abs(y)) * 32767))
 
 
+# ---------------------------------------------------------------- one GPU run per file
+# analyze_wav_file calls preprocess_audio (:1731), then _calculate_dynamic_noise_floor
+# on the envelope it returned (:1732), then _find_raw_peaks with that floor twice (the
+# preliminary pass :1635 and the main pass :1740, both via :89).  preprocess_audio
+# therefore runs every stage in one batch and keeps this thread's last recording; the
+# later calls are answered from it when their envelope is byte-identical to the one
+# returned, their parameters give the same detection settings and (for the peaks) the
+# height is that floor.  Anything else runs on the GPU as before.
+class _LastRecording(threading.local):
+    def __init__(self):
+        self.rec = None
+
+
+_last = _LastRecording()
+
+
+def _floor_key(params: Dict, sr: int):
+    return (sr, int(params["min_peak_distance_sec"] * sr), float(params["trough_prominence_quantile"]),
+            int(params["noise_window_sec"] * sr), float(params["noise_floor_quantile"]),
+            float(params.get("trough_rejection_multiplier", 4.0)))
+
+
+def _peak_key(params: Dict, sr: int):
+    return (sr, int(params["min_peak_distance_sec"] * sr), float(params["peak_prominence_quantile"]))
+
+
+def _same_bytes(a: np.ndarray, b: np.ndarray) -> bool:
+    return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+def _cached(env: np.ndarray, sr: int, key_name: str, key) -> dict:
+    rec = _last.rec
+    if rec is None or rec[key_name] != key or not _same_bytes(rec["env"], env):
+        return None
+    return rec
+
+
 def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: str = None,
                      device: int = 0) -> Tuple[np.ndarray, int]:
     """Reads, filters, and prepares the audio envelope for analysis (on the GPU).
 
     ``mode`` (or ``params["bpmx_mode"]`` when called through the reference's
     unchanged ``analyze_wav_file``): "reference" (default, bit-exact with the
-    shipped pipeline) or "native" (sosfiltfilt at fs -> decimate -> |hilbert|)."""
+    shipped pipeline) or "native" (sosfiltfilt at fs -> decimate -> |hilbert|).
+    The noise floor, troughs and raw peaks of the same recording are computed
+    in the same GPU run and kept for the calls that follow (see _LastRecording)."""
     if mode is None:
         mode = params.get("bpmx_mode", "reference")
     save_debug_file = params["save_filtered_wav"]
@@ -77,13 +117,20 @@ def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: 
     n = audio.shape[0]
     if -(-n // d.ds) <= 15:
         raise ValueError(PADLEN_MSG)
-    r = default_detector(device).run_host([audio], sample_rate, params, mode=mode, stages=N.STAGE_ENVELOPE,
+    _last.rec = None
+    stages = N.STAGE_ALL if d.distance >= 1 else N.STAGE_ENVELOPE     # distance < 1 raises in the later calls
+    r = default_detector(device).run_host([audio], sample_rate, params, mode=mode, stages=stages,
                                           want_y=bool(save_debug_file))[0]
     if save_debug_file:
         _write_debug_wav(f"{os.path.splitext(file_path)[0]}_filtered_debug.wav", d.sr, r["y"])
         base = os.path.basename(os.path.splitext(file_path)[0])
         _write_debug_wav(os.path.join(output_directory, f"{base}_filtered_debug.wav"), d.sr, r["y"])
-    return np.array(r["env"]), d.sr
+    env = np.array(r["env"])
+    if stages == N.STAGE_ALL:
+        _last.rec = {"env": env.copy(), "floor_key": _floor_key(params, d.sr), "peak_key": _peak_key(params, d.sr),
+                     "floor": np.array(r["floor"]), "troughs": np.array(r["troughs"]), "peaks": np.array(r["peaks"]),
+                     "flags": r["flags"], "n_raw_troughs": r["n_raw_troughs"]}
+    return env, d.sr
 
 
 def _series(values: np.ndarray):
@@ -96,7 +143,9 @@ def _calculate_dynamic_noise_floor(audio_envelope: np.ndarray, sample_rate: int,
     env = np.ascontiguousarray(audio_envelope, dtype=np.float64)
     if int(params["min_peak_distance_sec"] * sample_rate) < 1:
         raise ValueError(DISTANCE_MSG)
-    r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_FLOOR)[0]
+    r = _cached(env, sample_rate, "floor_key", _floor_key(params, sample_rate))
+    if r is None:
+        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_FLOOR)[0]
     fl = r["flags"]
     if fl & N.F_BAD_WINDOW:
         raise _window_error(params, sample_rate)
@@ -117,7 +166,9 @@ def find_raw_peaks(audio_envelope: np.ndarray, sample_rate: int, params: Dict, h
     if int(params["min_peak_distance_sec"] * sample_rate) < 1:
         raise ValueError(DISTANCE_MSG)
     floor = np.ascontiguousarray(np.broadcast_to(np.asarray(height_threshold, dtype=np.float64), env.shape))
-    r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor])[0]
+    r = _cached(env, sample_rate, "peak_key", _peak_key(params, sample_rate))
+    if r is None or not _same_bytes(r["floor"], floor):
+        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor])[0]
     peaks = np.array(r["peaks"], dtype=np.int64)
     logging.info(f"Found {len(peaks)} raw peaks using dynamic height threshold.")
     return peaks
@@ -183,6 +234,8 @@ def analyze_wav_files(file_paths: Sequence[str], params: Dict, output_directory:
                 raise ValueError(DISTANCE_MSG)
             res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save)
         except (ValueError, N.BpmxError) as exc:      # reported per file, as the GUI loop does (gui.py:247-251)
+            if isinstance(exc, N.BpmxError) and not exc.per_file:
+                raise                                 # HIP / device failure: not a per-file error
             for k in idx:                             # (a too-short file fails first, in filtfilt)
                 short = -(-audio[k][1].shape[0] // d.ds) <= 15
                 out[k] = {"error": ValueError(PADLEN_MSG) if short else exc}

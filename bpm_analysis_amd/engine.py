@@ -87,7 +87,15 @@ class Result:
 
 
 class Detector:
-    """One libbpmx context on one GPU.  Not shared across threads without the lock."""
+    """One libbpmx context on one GPU.
+
+    Threading (the reference is called from a GUI worker thread, gui.py:181-187,
+    and Gradio may call concurrently): ``run`` enqueues under ``lock`` on the
+    caller's current stream; the host entry points (``run_host``,
+    ``run_env_host``) hold the lock from upload to download on the detector's
+    own stream, so a context's scratch is never shared by two calls in flight.
+    ``default_detector`` gives each thread its own Detector (context + stream),
+    so concurrent threads also run concurrently on the GPU."""
 
     def __init__(self, device: int = 0):
         torch = _torch()
@@ -100,7 +108,8 @@ class Detector:
         ctx = ctypes.c_void_p()
         N.check(self.L.bpmx_create(device, ctypes.byref(ctx)), "bpmx_create")
         self.ctx = ctx
-        self.lock = threading.Lock()
+        self.lock = threading.RLock()
+        self._stream = None
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -114,6 +123,12 @@ class Detector:
             pass
 
     # ------------------------------------------------------------------ #
+    def host_stream(self):
+        """The stream of the host entry points (created on first use)."""
+        if self._stream is None:
+            self._stream = _torch().cuda.Stream(self.device)
+        return self._stream
+
     def stream_handle(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
 
@@ -205,6 +220,15 @@ class Detector:
             out[name] = (int(cnt), float(ms))
         return out
 
+    def stats(self) -> dict:
+        """Path counters of the last run with options | OPT_STATS (bpmx_stats)."""
+        buf = (ctypes.c_int64 * N.NSTATS)()
+        rc = self.L.bpmx_stats(self.ctx, buf, N.NSTATS)
+        if rc < 0:
+            N.check(rc, "bpmx_stats")
+        return {"raw_troughs": int(buf[N.STAT_RAW_TROUGHS]), "undecided": int(buf[N.STAT_UNDECIDED]),
+                "full_draft_chunks": int(buf[N.STAT_FULL_DRAFT])}
+
     # ------------------------------------------------------------------ #
     def run_host(self, recordings: List[np.ndarray], fs: int, params: dict, mode: str = "reference",
                  stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False,
@@ -234,11 +258,13 @@ class Detector:
         fo = np.zeros(len(recordings) + 1, dtype=np.int64)
         fo[1:] = np.cumsum([r.shape[0] for r in recordings])
         host = np.concatenate([np.ascontiguousarray(r).reshape(-1) for r in recordings])
-        pcm = torch.from_numpy(host).to(self.device)
-        res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log,
-                       options=options)
-        torch.cuda.synchronize(self.device)
-        return res.to_host()
+        with self.lock, torch.cuda.stream(self.host_stream()):
+            pcm = torch.from_numpy(host).to(self.device)
+            res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log,
+                           options=options)
+            out = res.to_host()          # .cpu() waits for this stream only
+            self.host_stream().synchronize()
+        return out
 
     def run_env_host(self, envs: List[np.ndarray], sr: int, params: dict, stages: int,
                      floors: Optional[List[np.ndarray]] = None, options: int = 0) -> List[dict]:
@@ -247,13 +273,15 @@ class Detector:
         fo = np.zeros(len(envs) + 1, dtype=np.int64)
         fo[1:] = np.cumsum([len(e) for e in envs])   # ds = 1: offsets == decimated offsets
         d = detect_design(sr, params)
-        out = self.alloc(fo, 1, d.sr)
-        out.env.copy_(torch.from_numpy(np.concatenate(envs).astype(np.float64)).to(self.device))
-        if floors is not None:
-            out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
-        self.run(None, fo, d.sr, params, stages=stages, out=out, d=d, options=options)
-        torch.cuda.synchronize(self.device)
-        return out.to_host()
+        with self.lock, torch.cuda.stream(self.host_stream()):
+            out = self.alloc(fo, 1, d.sr)
+            out.env.copy_(torch.from_numpy(np.concatenate(envs).astype(np.float64)).to(self.device))
+            if floors is not None:
+                out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
+            self.run(None, fo, d.sr, params, stages=stages, out=out, d=d, options=options)
+            res = out.to_host()
+            self.host_stream().synchronize()
+        return res
 
 
 def _torch_np_map():
@@ -262,12 +290,18 @@ def _torch_np_map():
             np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
 
 
-_default = {}
-_default_lock = threading.Lock()
+class _PerThread(threading.local):
+    def __init__(self):
+        self.dets = {}
+
+
+_default = _PerThread()
 
 
 def default_detector(device: int = 0) -> Detector:
-    with _default_lock:
-        if device not in _default:
-            _default[device] = Detector(device)
-        return _default[device]
+    """This thread's Detector on `device` (created on first use, in this thread:
+    gui.py runs the analysis on a daemon worker thread, gui.py:181-187)."""
+    det = _default.dets.get(device)
+    if det is None:
+        det = _default.dets[device] = Detector(device)
+    return det

@@ -96,6 +96,8 @@ def _detect_local(items, idx, fs, params, mode, detector):
                 raise ValueError(DISTANCE_MSG)
             out = detector.run_host([data[i][1] for i in ids], f, params, mode=mode, stages=N.STAGE_ALL)
         except (ValueError, N.BpmxError) as exc:
+            if isinstance(exc, N.BpmxError) and not exc.per_file:
+                raise                                   # HIP / device failure: the rank fails, not the files
             for i in ids:
                 short = d is not None and -(-data[i][1].shape[0] // d.ds) <= 15
                 res[i] = {"error": ValueError(PADLEN_MSG) if short else exc}

@@ -93,8 +93,17 @@ enum bpmx_option {
     BPMX_OPT_HILBERT_R2C = 512,  /* native mode, recordings outside the fused Hilbert kernel: one rocFFT
                                     R2C/C2R plan per distinct length instead of the batched Bluestein
                                     transform (test/diagnostic) */
-    BPMX_OPT_REF_SERIAL_MEAN = 1024  /* reference mode: form the rolling mean's outputs inside the sequential
+    BPMX_OPT_REF_SERIAL_MEAN = 1024, /* reference mode: form the rolling mean's outputs inside the sequential
                                         pass instead of from its running sums in parallel (test/diagnostic) */
+    BPMX_OPT_STATS = 2048            /* count the run's path decisions for bpmx_stats (diagnostic) */
+};
+
+/* bpmx_stats counters of the last run with BPMX_OPT_STATS */
+enum bpmx_stat {
+    BPMX_STAT_RAW_TROUGHS = 0,   /* raw troughs of the recordings whose draft floor was bracketed */
+    BPMX_STAT_UNDECIDED = 1,     /* of those, troughs the bracket left open: draft evaluated there exactly */
+    BPMX_STAT_FULL_DRAFT = 2,    /* trough chunks whose recording fell back to the whole draft floor */
+    BPMX_NSTATS = 8
 };
 
 typedef struct bpmx_ctx bpmx_ctx;
@@ -174,6 +183,11 @@ int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len);
  * launch), so a timed run can carry one kernel's device time without
  * bracketing every launch. */
 int bpmx_profile_only(bpmx_ctx *ctx, const char *label);
+
+/* Counters (enum bpmx_stat) of the last bpmx_run on ctx that had
+ * BPMX_OPT_STATS set: waits for that run, copies min(n, BPMX_NSTATS) of them
+ * into out (zeros if none), returns BPMX_NSTATS or an error code. */
+int bpmx_stats(bpmx_ctx *ctx, int64_t *out, int n);
 
 #ifdef __cplusplus
 }

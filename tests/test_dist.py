@@ -182,3 +182,47 @@ def test_two_rank_sharded_runner_gathers_peaks_and_bpm_curves(stages):
         assert np.array_equal(r["bpm_times"], np.asarray(m["bpm_times"]))
         assert np.array_equal(r["bpm"], m["smoothed_bpm"].values)
         assert r["flags"] == o["flags"] and len(r["bpm"]) > 5
+
+
+def _bench_json(stdout: str) -> dict:
+    import json
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("workload", ["metric", "c5"])
+def test_bench_launches_n_ranks(workload):
+    """`python bench.py --gpus 2` starts two ranks itself (torch.distributed.run
+    child, gloo under --cpu-stub), reports n_gpus 2 and gathers both ranks'
+    files to rank 0; parity and the CPU baseline are kept at N > 1."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--cpu-stub", "--steps", "1", "--warmup", "1"]
+    if workload == "metric":
+        cmd += ["--files", "3", "--secs", "6", "--parity-files", "2", "--host-beat-files", "1"]
+    else:   # 5 recordings of 10-30 min at 96 kHz stereo are too much oracle work: shrink via the chunk budget only
+        cmd += ["--workload", "c5", "--c5-files", "2", "--c5-parity-files", "1", "--c5-chunk-gb", "0.001"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _bench_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["data"].startswith("cpu-stub")
+    assert line["parity"]["ok"] and line["parity"]["ranks"] == 2
+    if workload == "metric":
+        assert line["result_gather"]["files"] == 6 and line["result_gather"]["ranks_seen"] == [0, 1]
+        assert line["cpu_baseline"]["per_rank"] and line["cpu_baseline"]["rank"] == 0
+        assert line["parity"]["files"] == 4
+    else:
+        assert line["result_gather"]["files"] == 2 and line["scaling"] == "strong"
+
+
+def test_bench_refuses_world_mismatch():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--cpu-stub"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=repo)
+    assert r.returncode != 0 and "refusing" in r.stderr

@@ -812,3 +812,145 @@ def test_chunked_wavelet_matrix_on_long_recordings(det):
         of, ot, _ = O.noise_floor(env, d, params)
         assert _same(ra["floor"], of)
         assert _same(ra["troughs"], ot)
+
+
+@pytest.mark.parametrize("mult", [4.0, 2.0, 1.5, 1.0, 0.7])
+def test_draft_point_resolves_undecided_troughs(det, mult):
+    """Troughs the draft bracket leaves open are decided from the exact draft
+    value at the trough (draft_point: one wave per trough), not by computing the
+    whole draft floor: bit-identical floors, troughs and peaks to
+    BPMX_OPT_DRAFT_FULL and to the oracle, with no recording sent to the full
+    draft.  Lower rejection multipliers put many troughs near the threshold
+    (vulpine leaves 241 of 1456 undecided at the default 4.0)."""
+    from bpm_analysis_amd import _native as N
+    params = dict(G.BASE_PARAMS, trough_rejection_multiplier=mult)
+    und = raw = 0
+    for env, sr in _floor_envelopes():
+        a = det.run_env_host([env], sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS, options=N.OPT_STATS)[0]
+        st = det.stats()
+        und += st["undecided"]
+        raw += st["raw_troughs"]
+        assert st["full_draft_chunks"] == 0
+        b = det.run_env_host([env], sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS, options=N.OPT_DRAFT_FULL)[0]
+        for k in ("floor", "troughs", "peaks"):
+            assert _same(a[k], b[k]), k
+        assert a["flags"] == b["flags"]
+        d = O.derive(sr, params)
+        of, ot, ofl = O.noise_floor(env, d, params)
+        assert _same(a["floor"], of) and _same(a["troughs"], ot) and (a["flags"] & 7) == ofl
+    assert raw > 0
+    if mult <= 2.0:
+        assert und > 0.05 * raw            # the pointwise path is really exercised
+
+
+def _golden_wav(tmp_path, name):
+    from scipy.io import wavfile
+    g = G.load(name)
+    wav = tmp_path / f"{name}.wav"
+    wavfile.write(str(wav), int(g["fs"]), g["pcm"])
+    return g, str(wav)
+
+
+def test_dropin_one_gpu_run_per_file(det, tmp_path, monkeypatch):
+    """analyze_wav_file's call sequence (preprocess_audio -> noise floor ->
+    _find_raw_peaks twice, bpm_analysis.py:1731-1740, :89) costs one GPU run:
+    the floor and peak calls are answered from the run preprocess_audio made,
+    bit-exact; a changed envelope or height goes to the GPU again."""
+    from bpm_analysis_amd import dropin
+    from bpm_analysis_amd.engine import Detector
+    g, wav = _golden_wav(tmp_path, "ref_44k_60s_mono")
+    params = dict(g["params"], save_filtered_wav=False)
+    env, sr = dropin.preprocess_audio(wav, params, str(tmp_path))
+    calls = []
+    orig = Detector.run_env_host
+    monkeypatch.setattr(Detector, "run_env_host", lambda self, *a, **k: calls.append(1) or orig(self, *a, **k))
+    floor, troughs = dropin._calculate_dynamic_noise_floor(env, sr, params)
+    p1 = dropin.find_raw_peaks(env, sr, params, floor.values)
+    p2 = dropin.find_raw_peaks(env, sr, dict(params, pairing_confidence_threshold=0.75), floor.values)
+    assert calls == []
+    assert _same(env, g["env"]) and _same(floor.values, g["floor"]) and _same(troughs, g["troughs"])
+    assert _same(p1, g["peaks"]) and _same(p2, g["peaks"])
+    # a different height or envelope is computed on the GPU
+    p3 = dropin.find_raw_peaks(env, sr, params, floor.values * 1.5)
+    env2 = env.copy()
+    env2[100] += 1.0
+    dropin._calculate_dynamic_noise_floor(env2, sr, params)
+    assert len(calls) == 2
+    want = O.raw_peaks(g["env"], g["floor"] * 1.5, O.derive(sr, params), params)
+    assert _same(p3, want)
+
+
+def test_dropin_first_detector_on_a_daemon_thread(tmp_path):
+    """gui.py:181-187 imports and runs analyze_wav_file on a daemon thread, so the
+    first GPU context is created there: the patched reference entry point runs
+    there bit-exact, and the main thread never touches the GPU (own process)."""
+    import subprocess
+    import sys
+    g, wav = _golden_wav(tmp_path, "ref_44k_60s_mono")
+    np.savez(str(tmp_path / "want.npz"), env=g["env"], floor=g["floor"], troughs=g["troughs"], peaks=g["peaks"])
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys, threading
+import numpy as np
+sys.path.insert(0, {repo!r})
+from tests.test_gpu_parity import _stand_in_reference
+from tests import goldens as G
+from bpm_analysis_amd import dropin, engine
+mod = _stand_in_reference()
+dropin.patch_reference(mod)
+params = dict(G.load("ref_44k_60s_mono")["params"], save_filtered_wav=False)
+res = {{}}
+def work():
+    try:
+        res["out"] = mod.analyze_wav_file({wav!r}, params, None, {wav!r}, {str(tmp_path)!r})
+        res["dets"] = len(engine._default.dets)
+    except BaseException as exc:
+        res["err"] = repr(exc)
+t = threading.Thread(target=work, daemon=True)
+t.start()
+t.join(300)
+assert "err" not in res, res.get("err")
+assert res["dets"] == 1 and len(engine._default.dets) == 0
+w = np.load({str(tmp_path / "want.npz")!r})
+env, floor, troughs, peaks = res["out"]
+for a, b in ((env, w["env"]), (floor.values, w["floor"]), (troughs, w["troughs"]), (peaks, w["peaks"])):
+    assert np.array_equal(np.asarray(a), b, equal_nan=True)
+print("daemon-thread ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "daemon-thread ok" in r.stdout, r.stderr[-3000:]
+
+
+def test_dropin_two_threads_at_once(det, tmp_path):
+    """Two threads run the patched reference entry point at the same time on
+    different files (Gradio may call concurrently; each thread gets its own
+    context and stream), several times each: every result bit-exact."""
+    import threading
+    from bpm_analysis_amd import dropin
+    mod = _stand_in_reference()
+    dropin.patch_reference(mod)
+    cases = [_golden_wav(tmp_path, n) for n in ("ref_44k_60s_mono", "ref_48k_20s_mono")]
+    bar = threading.Barrier(2)
+    errs = []
+
+    def work(g, wav):
+        try:
+            params = dict(g["params"], save_filtered_wav=False)
+            for _ in range(4):
+                bar.wait(timeout=120)
+                env, floor, troughs, peaks = mod.analyze_wav_file(wav, params, None, wav, str(tmp_path))
+                assert _same(env, g["env"]) and _same(floor.values, g["floor"])
+                assert _same(troughs, g["troughs"]) and _same(peaks, g["peaks"])
+                # and the batched entry on the other file's rate group at the same time
+                r = dropin.analyze_batch([g["pcm"]], int(g["fs"]), params)[0]
+                assert _same(r["peaks"], g["peaks"])
+        except BaseException as exc:          # noqa: BLE001 - reported below
+            errs.append(repr(exc))
+            bar.abort()
+
+    ts = [threading.Thread(target=work, args=c) for c in cases]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    assert not errs, errs

@@ -18,15 +18,17 @@ for step in "$@"; do
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    c5) run bench_c5 600 python bench.py --workload c5 --steps 5 --warmup 2 ;;
+    c5) run bench_c5 900 python bench.py --workload c5 --steps 5 --warmup 2 ;;
+    c5_64) run bench_c5_64 600 python bench.py --workload c5 --c5-files 64 --steps 5 --warmup 2 ;;
+    gputest) run pytest_gpu_sel 600 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread -k "${GPUTEST_K:-draft}" ;;
     bench_ref) run bench_ref 600 python bench.py --steps 10 --warmup 2 --mode reference ;;
-    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 ;;
-    rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --mode reference ;;
-    rocprof_ref_mc) run rocprof_ref_mc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_ref_mc -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 4 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --mode reference ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 ;;
-    pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --mode reference ;;
-    pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --mode reference ;;
+    rocprof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 ;;
+    rocprof_ref) run rocprof_ref 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace_ref -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
+    rocprof_ref_mc) run rocprof_ref_mc 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_ref_mc -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 4 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 ;;
+    pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
+    pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
