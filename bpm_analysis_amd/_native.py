@@ -37,7 +37,7 @@ OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",
            "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only",
-           "bpmx_stats"]
+           "bpmx_stats", "bpmx_set_pipeline"]
 
 
 class Params(ctypes.Structure):
@@ -119,6 +119,8 @@ def load() -> ctypes.CDLL:
     L.bpmx_profile_only.restype = ctypes.c_int
     L.bpmx_stats.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     L.bpmx_stats.restype = ctypes.c_int
+    L.bpmx_set_pipeline.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.bpmx_set_pipeline.restype = ctypes.c_int
     if L.bpmx_abi_version() != ABI_VERSION:
         raise BpmxError(f"libbpmx ABI {L.bpmx_abi_version()} != expected {ABI_VERSION}; rebuild")
     _lib = L

@@ -123,6 +123,10 @@ void bpmx_destroy(bpmx_ctx *ctx) {
         if (ctx->side_join[i]) (void)hipEventDestroy(ctx->side_join[i]);
     }
     if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
+    for (bpmx_ctx *c : ctx->pipe_sub) bpmx_destroy(c);
+    if (ctx->pipe_env) (void)hipStreamDestroy(ctx->pipe_env);
+    if (ctx->pipe_det) (void)hipStreamDestroy(ctx->pipe_det);
+    for (auto e : ctx->pipe_ev) (void)hipEventDestroy(e);
     delete ctx;
 }
 
@@ -239,7 +243,8 @@ int bpmx_stats(bpmx_ctx *ctx, int64_t *out, int n) {
     return BPMX_NSTATS;
 }
 
-int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {
+static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream,
+                    bool env_active) {
     if (!ctx || !P || !B || !O) return fail(BPMX_E_ARG, "NULL argument");
     const int F = B->n_files;
     if (F < 1 || !B->frame_offsets) return fail(BPMX_E_ARG, "empty batch");
@@ -266,10 +271,12 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     int64_t *d_stats = nullptr;
     if (P->options & BPMX_OPT_STATS) {
         int src = BPMX_OK;
-        d_stats = (int64_t *)ctx->buf("stats", BPMX_NSTATS * 8, &src);
+        d_stats = (int64_t *)ctx->pr()->buf("stats", BPMX_NSTATS * 8, &src);
         if (src != BPMX_OK) return src;
-        HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
-        ctx->stats_stream = s;
+        if (!ctx->root) {                               /* a pipelined run zeroes them once */
+            HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
+            ctx->stats_stream = s;
+        }
     }
 
     /* ---- geometry ---- */
@@ -285,7 +292,7 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
         doff[f + 1] = doff[f] + nd;
         boff[f + 1] = boff[f] + (nd + 63) / 64;
         maxnd = std::max(maxnd, nd);
-        const bool ok = do_env ? nd > 15 : nd >= 1;
+        const bool ok = (do_env || env_active) ? nd > 15 : nd >= 1;
         active[f] = ok ? 1 : 0;
         if (nd >= (int64_t)INT_MAX / 2) return fail(BPMX_E_LIMIT, "recording too long");
     }
@@ -679,6 +686,157 @@ int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpm
     }
 #undef FIND_PEAKS
     return BPMX_OK;
+}
+
+/* ---------------------------------------------------------------------------
+ * Pipelined run (bpmx_set_pipeline): the batch in `chunks` runs of whole
+ * recordings.  Chunk k's envelope stage (native mode: the HBM-bound block
+ * kernel and the per-recording transforms) runs on an internal stream that may
+ * be restricted to `env_cus` CUs; its detection stages (quantiles, troughs,
+ * noise floor, peaks: latency-bound per-recording kernels) run on the caller's
+ * stream (or an internal one restricted to the other CUs) once its envelope is
+ * done, while chunk k+1's envelope streams its PCM.  Each chunk slot has its
+ * own contexts (scratch, geometry) for the two stages, so the only data the
+ * streams share are the output arrays, ordered by events.  Outputs are those
+ * of one run over the whole batch.
+ * ------------------------------------------------------------------------- */
+static int pipe_ready(bpmx_ctx *ctx, int K) {
+    if ((int)ctx->pipe_sub.size() < 2 * K) {
+        while ((int)ctx->pipe_sub.size() < 2 * K) {
+            bpmx_ctx *c = new bpmx_ctx();
+            c->device = ctx->device;
+            c->root = ctx;
+            ctx->pipe_sub.push_back(c);
+        }
+    }
+    while ((int)ctx->pipe_ev.size() < K + 1) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->pipe_ev.push_back(e);
+    }
+    auto mk = [&](hipStream_t *st, int lo, int ncu) -> int {
+        if (*st) return BPMX_OK;
+        int total = 0;
+        HIP_TRY(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        if (ncu <= 0 || ncu >= total) {
+            HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+            return BPMX_OK;
+        }
+        /* mask bits [lo, lo + ncu): the driver deals the bits of a stream's CU
+         * mask round-robin over the XCDs (bit c -> XCD c % 8, the (c / 8)-th CU
+         * there), so a contiguous run of a multiple of 8 bits keeps the same
+         * share of CUs on every XCD, as the workgroups are dealt too */
+        std::vector<uint32_t> mask((total + 31) / 32, 0u);
+        for (int c = lo; c < lo + ncu && c < total; ++c) mask[c / 32] |= 1u << (c % 32);
+        HIP_TRY(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+        return BPMX_OK;
+    };
+    int rc = mk(&ctx->pipe_env, 0, ctx->pipe_env_cus);
+    if (rc != BPMX_OK) return rc;
+    if (ctx->pipe_det_cus > 0 && (rc = mk(&ctx->pipe_det, ctx->pipe_env_cus, ctx->pipe_det_cus)) != BPMX_OK) return rc;
+    return BPMX_OK;
+}
+
+static size_t dtype_bytes(int dt) {
+    switch (dt) {
+    case BPMX_DT_U8: return 1;
+    case BPMX_DT_I16: return 2;
+    case BPMX_DT_F64: return 8;
+    default: return 4;
+    }
+}
+
+static int run_pipelined(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O,
+                         hipStream_t s) {
+    const int F = B->n_files;
+    const int K = std::min(ctx->pipe_chunks, F);
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = pipe_ready(ctx, K);
+    if (rc != BPMX_OK) return rc;
+    if (P->options & BPMX_OPT_STATS) {
+        int64_t *d_stats = (int64_t *)ctx->buf("stats", BPMX_NSTATS * 8, &rc);
+        if (rc != BPMX_OK) return rc;
+        HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
+        ctx->stats_stream = s;
+    }
+    /* chunk boundaries by frames (recordings are whole), decimated offsets */
+    const int64_t *fo = B->frame_offsets;
+    const int64_t total = fo[F] - fo[0];
+    std::vector<int> fb(K + 1, F);
+    fb[0] = 0;
+    for (int k = 1, f = 0; k < K; ++k) {
+        const int64_t want = fo[0] + total * k / K;
+        while (f < F && fo[f] < want) ++f;
+        fb[k] = std::max(fb[k - 1] + 1, std::min(f, F - (K - k)));
+    }
+    std::vector<int64_t> doff(F + 1, 0);
+    for (int f = 0; f < F; ++f) doff[f + 1] = doff[f] + bpmx_decimated_length(fo[f + 1] - fo[f], P->ds);
+    /* the envelope stream starts after everything already queued on the caller's stream */
+    hipEvent_t start = ctx->pipe_ev[K];
+    HIP_TRY(hipEventRecord(start, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->pipe_env, start, 0));
+    if (ctx->pipe_det) HIP_TRY(hipStreamWaitEvent(ctx->pipe_det, start, 0));
+    const size_t fbytes = dtype_bytes(P->dtype) * (size_t)P->channels;
+    bpmx_params pe = *P, pd = *P;
+    pe.stages = BPMX_STAGE_ENVELOPE;
+    pd.stages = P->stages & ~BPMX_STAGE_ENVELOPE;
+    for (int k = 0; k < K; ++k) {
+        const int f0 = fb[k], f1 = fb[k + 1];
+        bpmx_batch b;
+        b.n_files = f1 - f0;
+        b.reserved = 0;
+        b.pcm = (const char *)B->pcm + (size_t)(fo[f0] - fo[0]) * fbytes;
+        b.frame_offsets = fo + f0;
+        const int64_t d0 = doff[f0];
+        bpmx_out o;
+        o.env = O->env + d0;
+        o.floor = O->floor ? O->floor + d0 : nullptr;
+        o.y = O->y ? O->y + d0 : nullptr;
+        o.troughs = O->troughs ? O->troughs + d0 : nullptr;
+        o.peaks = O->peaks ? O->peaks + d0 : nullptr;
+        o.n_troughs = O->n_troughs + f0;
+        o.n_peaks = O->n_peaks + f0;
+        o.flags = O->flags + f0;
+        o.n_raw_troughs = O->n_raw_troughs ? O->n_raw_troughs + f0 : nullptr;
+        if ((rc = run_impl(ctx->pipe_sub[2 * k], &pe, &b, &o, ctx->pipe_env, true)) != BPMX_OK) return rc;
+        HIP_TRY(hipEventRecord(ctx->pipe_ev[k], ctx->pipe_env));
+        /* detection: the restricted stream while later envelopes run, the
+         * caller's stream for the last chunk (every CU free by then) */
+        hipStream_t sd = (ctx->pipe_det && k + 1 < K) ? ctx->pipe_det : s;
+        HIP_TRY(hipStreamWaitEvent(sd, ctx->pipe_ev[k], 0));
+        if (pd.stages && (rc = run_impl(ctx->pipe_sub[2 * k + 1], &pd, &b, &o, sd, true)) != BPMX_OK) return rc;
+    }
+    if (ctx->pipe_det) {
+        /* the caller's stream completes after every chunk's detection */
+        hipEvent_t done = ctx->pipe_ev[K];
+        HIP_TRY(hipEventRecord(done, ctx->pipe_det));
+        HIP_TRY(hipStreamWaitEvent(s, done, 0));
+    }
+    return BPMX_OK;
+}
+
+int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus) {
+    if (!ctx || ctx->root) return fail(BPMX_E_ARG, "bad context");
+    if (chunks < 0 || chunks > 64 || env_cus < 0 || det_cus < 0) return fail(BPMX_E_ARG, "bad pipeline shape");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (env_cus != ctx->pipe_env_cus || det_cus != ctx->pipe_det_cus) {
+        if (ctx->pipe_env) (void)hipStreamDestroy(ctx->pipe_env);
+        if (ctx->pipe_det) (void)hipStreamDestroy(ctx->pipe_det);
+        ctx->pipe_env = ctx->pipe_det = nullptr;
+    }
+    ctx->pipe_chunks = chunks;
+    ctx->pipe_env_cus = env_cus;
+    ctx->pipe_det_cus = det_cus;
+    return BPMX_OK;
+}
+
+int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {
+    if (ctx && P && B && O && !ctx->root && ctx->pipe_chunks >= 2 && B->n_files >= 2 * ctx->pipe_chunks &&
+        (P->stages & BPMX_STAGE_ENVELOPE) && (P->stages & (BPMX_STAGE_FLOOR | BPMX_STAGE_PEAKS)) &&
+        B->frame_offsets && B->pcm && O->env && O->n_troughs && O->n_peaks && O->flags)
+        return run_pipelined(ctx, P, B, O, (hipStream_t)stream);
+    return run_impl(ctx, P, B, O, stream, false);
 }
 
 }  // extern "C"

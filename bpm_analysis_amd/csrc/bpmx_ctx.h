@@ -25,6 +25,15 @@ int fail(int code, const std::string &msg);
 
 struct bpmx_ctx {
     int device = 0;
+    /* pipelined runs (bpmx_set_pipeline): per chunk slot one context for the
+     * envelope stage and one for detection, each with its own scratch and
+     * geometry; they profile into the root context */
+    bpmx_ctx *root = nullptr;
+    int pipe_chunks = 0, pipe_env_cus = 0, pipe_det_cus = 0;
+    std::vector<bpmx_ctx *> pipe_sub;              /* [2 * chunks]: env, det per slot */
+    hipStream_t pipe_env = nullptr, pipe_det = nullptr;
+    std::vector<hipEvent_t> pipe_ev;               /* [chunks + 1]: envelope k done, start fork */
+    bpmx_ctx *pr() { return root ? root : this; }
     std::map<std::string, std::pair<void *, size_t>> bufs;
     std::vector<int64_t> g_key;   /* geometry of the last upload */
     /* native-mode block-state tables (host copies back the async uploads) */
@@ -97,7 +106,7 @@ struct Launch {
     const char *name;
     hipEvent_t a = nullptr, b = nullptr;
     bool on() const { return ctx->prof && (ctx->prof_only.empty() || ctx->prof_only == name); }
-    Launch(bpmx_ctx *c, hipStream_t st, const char *n) : ctx(c), s(st), name(n) {
+    Launch(bpmx_ctx *c, hipStream_t st, const char *n) : ctx(c->pr()), s(st), name(n) {
         if (on()) { a = ctx->ev(); (void)hipEventRecord(a, s); }
     }
     int done() {

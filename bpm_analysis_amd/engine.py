@@ -220,6 +220,10 @@ class Detector:
             out[name] = (int(cnt), float(ms))
         return out
 
+    def set_pipeline(self, chunks: int, env_cus: int = 0, det_cus: int = 0):
+        """bpmx_set_pipeline: overlap chunk k's envelope with chunk k-1's detection (0 = off)."""
+        N.check(self.L.bpmx_set_pipeline(self.ctx, chunks, env_cus, det_cus), "bpmx_set_pipeline")
+
     def stats(self) -> dict:
         """Path counters of the last run with options | OPT_STATS (bpmx_stats)."""
         buf = (ctypes.c_int64 * N.NSTATS)()

@@ -184,6 +184,16 @@ int bpmx_profile_read(bpmx_ctx *ctx, char *buf, int len);
  * bracketing every launch. */
 int bpmx_profile_only(bpmx_ctx *ctx, const char *label);
 
+/* Pipelined runs: batches of at least 2 * chunks recordings with ENVELOPE and
+ * a detection stage run as `chunks` consecutive groups of recordings; group
+ * k's envelope runs on an internal stream restricted to env_cus CUs (0: no
+ * restriction) while group k-1's detection runs beside it (on an internal
+ * stream restricted to det_cus other CUs when det_cus > 0, else on the
+ * caller's stream), so the HBM-bound envelope kernels overlap the
+ * latency-bound detection kernels.  Same outputs as an unpipelined run.
+ * chunks = 0 (the default) turns it off.  Waits for the device. */
+int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus);
+
 /* Counters (enum bpmx_stat) of the last bpmx_run on ctx that had
  * BPMX_OPT_STATS set: waits for that run, copies min(n, BPMX_NSTATS) of them
  * into out (zeros if none), returns BPMX_NSTATS or an error code. */

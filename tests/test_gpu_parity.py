@@ -954,3 +954,34 @@ def test_dropin_two_threads_at_once(det, tmp_path):
     for t in ts:
         t.join(600)
     assert not errs, errs
+
+
+def test_config_c5_shard_of_eight(det):
+    """BASELINE config C5 at its stated recording shape: a shard of 8 ragged
+    U[10, 30] min 96 kHz stereo int16 recordings (bench.c5_lengths, the
+    bench's own seeds) in one device batch, longest first, native mode; the
+    four shortest checked against the oracle (indices exact, envelope and
+    floor within 1e-9 of scale) and every recording's peaks sane."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    import bench
+    fs, ch = 96000, 2
+    lengths = bench.c5_lengths(8, fs)
+    order = np.argsort(-lengths, kind="stable")
+    lens = lengths[order]
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    seeds = [100_000 + int(i) for i in order]
+    pcm = det.synth(fo, fs, ch, seeds=seeds)
+    params = dict(G.BASE_PARAMS)
+    res = det.run(pcm, fo, fs, params, mode="native", channels=ch)
+    torch.cuda.synchronize()
+    host = res.to_host()
+    del pcm
+    check = list(range(len(lens)))[-4:]                  # the four shortest
+    with ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(lambda k: O.detect(O.synth(seeds[k], int(lens[k]), fs, ch), fs, params, mode="native"),
+                           check))
+    for k, o in zip(check, outs):
+        _check_file(host[k], o, exact_env=False)
+    for h, n in zip(host, lens):
+        assert len(h["env"]) == -(-int(n) // 300) and len(h["peaks"]) > 10 * (n // fs // 60)

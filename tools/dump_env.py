@@ -1,4 +1,7 @@
-"""Write gpurun_out/env.bin: native-mode envelopes of the bench workload (for tools/fpbench)."""
+"""Write gpurun_out/env.bin: envelopes of the bench workload (for tools/fpbench).
+
+    python tools/dump_env.py [F] [native|reference] [out path]
+"""
 import os
 import sys
 
@@ -13,11 +16,13 @@ det = Detector(0)
 fo = np.arange(F + 1, dtype=np.int64) * n
 pcm = det.synth(fo, fs, 1, seed0=0)
 params = dict(DEFAULT_PARAMS)
-res = det.run(pcm, fo, fs, params, mode="native", stages=N.STAGE_ENVELOPE)
+mode = sys.argv[2] if len(sys.argv) > 2 else "native"
+res = det.run(pcm, fo, fs, params, mode=mode, stages=N.STAGE_ENVELOPE)
 env = res.env.cpu().numpy()
 nd = len(env) // F
 os.makedirs("gpurun_out", exist_ok=True)
-with open("gpurun_out/env.bin", "wb") as fh:
+path = sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/env.bin"
+with open(path, "wb") as fh:
     np.array([F, nd], dtype=np.int64).tofile(fh)
     env.astype(np.float64).tofile(fh)
 print("wrote", F, nd)

@@ -29,6 +29,11 @@ for step in "$@"; do
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 ;;
     pmc_ref_fetch) run pmc_ref_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_ref_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
     pmc_ref_write) run pmc_ref_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_ref_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 --mode reference ;;
+    lanebench) run lanebench 120 ./tools/lanebench ;;
+    pipesweep) run pipesweep 600 python tools/pipe_sweep.py --steps 10 ;;
+    pipesweep_ref) run pipesweep_ref 600 python tools/pipe_sweep.py --steps 5 --mode reference --shapes 0,0,0 4,0,0 4,192,0 0,0,0 ;;
+    fpref) run dump_env_ref 300 python tools/dump_env.py 1024 reference /tmp/env_ref.bin && run fpbench_ref 120 ./tools/fpbench /tmp/env_ref.bin l ;;
+    fpnat) run dump_env_nat 300 python tools/dump_env.py 1024 native /tmp/env_nat.bin && run fpbench_nat 120 ./tools/fpbench /tmp/env_nat.bin l ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
