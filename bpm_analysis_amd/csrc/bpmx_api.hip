@@ -18,6 +18,7 @@
 #include <climits>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <vector>
@@ -124,6 +125,7 @@ void bpmx_destroy(bpmx_ctx *ctx) {
     }
     if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
     for (bpmx_ctx *c : ctx->pipe_sub) bpmx_destroy(c);
+    bpmx::longfft_free(ctx);
     if (ctx->pipe_env) (void)hipStreamDestroy(ctx->pipe_env);
     if (ctx->pipe_det) (void)hipStreamDestroy(ctx->pipe_det);
     for (auto e : ctx->pipe_ev) (void)hipEventDestroy(e);
@@ -340,19 +342,24 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.scratch = scr; a.env = O->env; a.y = O->y;
             /* chain mode (the rolling mean's outputs formed in parallel afterwards) */
             const bool chain = !(P->options & BPMX_OPT_REF_SERIAL_MEAN) && P->env_window > 1;
-            a.sums = chain ? (double *)ctx->buf("ref_sums", (size_t)std::max<int64_t>(maxnd, 1) * F * 8, &rc) : nullptr;
+            a.sums = chain ? (double *)ctx->buf("ref_sums", (size_t)(std::max<int64_t>(maxnd, 1) + 1) * F * 8, &rc) : nullptr;
             a.chain = (int32_t *)ctx->buf("ref_chain", (size_t)F * 4, &rc);
             if (rc != BPMX_OK) return rc;
             const bool multi = P->channels > 1;
             const dim3 g((F + 63) / 64), b(64);
             const dim3 gp((unsigned)((maxnd + 30 + 63) / 64), (unsigned)((F + 63) / 64));
+            /* b1 = b3 = 0 with integer PCM (always finite): the filter step
+             * skips the two zero products (k_envelope_ref.hip, Df2t::step) */
+            const bool zb = P->ba_b[1] == 0.0 && P->ba_b[3] == 0.0 &&
+                            (P->dtype == BPMX_DT_U8 || P->dtype == BPMX_DT_I16 || P->dtype == BPMX_DT_I32);
+#define ENV_REF_K(DT, M, Z) LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, M, Z>), g, b, 0, s, a)
 #define ENV_REF(DT)                                                                                  \
     if (multi) {                                                                                     \
         LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, true>), gp, dim3(256), 0, s, a);                 \
-        LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, true>), g, b, 0, s, a);               \
+        if (zb && DT <= BPMX_DT_I32) ENV_REF_K(DT, true, DT <= BPMX_DT_I32); else ENV_REF_K(DT, true, false); \
     } else {                                                                                         \
         LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, false>), gp, dim3(256), 0, s, a);                \
-        LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, false>), g, b, 0, s, a);              \
+        if (zb && DT <= BPMX_DT_I32) ENV_REF_K(DT, false, DT <= BPMX_DT_I32); else ENV_REF_K(DT, false, false); \
     }
             switch (P->dtype) {
             case BPMX_DT_U8: ENV_REF(BPMX_DT_U8) break;
@@ -362,6 +369,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             default: ENV_REF(BPMX_DT_F64) break;
             }
 #undef ENV_REF
+#undef ENV_REF_K
             if (chain)
                 LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean, dim3((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64)),
                        dim3(256), 0, s, a);
@@ -727,7 +735,14 @@ static int pipe_ready(bpmx_ctx *ctx, int K) {
          * there), so a contiguous run of a multiple of 8 bits keeps the same
          * share of CUs on every XCD, as the workgroups are dealt too */
         std::vector<uint32_t> mask((total + 31) / 32, 0u);
-        for (int c = lo; c < lo + ncu && c < total; ++c) mask[c / 32] |= 1u << (c % 32);
+        if (std::getenv("BPMX_CUMASK_PER_WORD")) {
+            /* diagnostic: the other reading, one 32-bit word per XCD */
+            const int X = (total + 31) / 32;
+            for (int x = 0; x < X; ++x)
+                for (int c = lo / X; c < (lo + ncu) / X && c < 32; ++c) mask[x] |= 1u << c;
+        } else {
+            for (int c = lo; c < lo + ncu && c < total; ++c) mask[c / 32] |= 1u << (c % 32);
+        }
         HIP_TRY(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
         return BPMX_OK;
     };

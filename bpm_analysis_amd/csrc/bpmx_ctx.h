@@ -34,6 +34,7 @@ struct bpmx_ctx {
     hipStream_t pipe_env = nullptr, pipe_det = nullptr;
     std::vector<hipEvent_t> pipe_ev;               /* [chunks + 1]: envelope k done, start fork */
     bpmx_ctx *pr() { return root ? root : this; }
+    void *lf = nullptr;                            /* k_longfft.hip's plan state (LfHost) */
     std::map<std::string, std::pair<void *, size_t>> bufs;
     std::vector<int64_t> g_key;   /* geometry of the last upload */
     /* native-mode block-state tables (host copies back the async uploads) */

@@ -251,7 +251,7 @@ __host__ __device__ inline size_t rollq_lds_bytes(int T, int cap) {
 }
 constexpr int RQ_T = 256;   /* outputs per tile = threads per workgroup */
 
-template <int DT, bool MULTI>
+template <int DT, bool MULTI, bool ZB>
 __global__ void k_envelope_ref_t(EnvRefArgs A);
 template <int DT, bool MULTI>
 __global__ void k_ref_pick(EnvRefArgs A);

@@ -15,6 +15,11 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
 /* k_bluestein.hip: hb = N * Hilbert transform of yd for the listed recordings */
 /* rocfft_setup() exactly once per process (std::call_once), whatever thread gets there first */
 int rocfft_setup_once();
+/* k_longfft.hip: exact-length four-step Hilbert of long recordings */
+bool longfft_supported(int64_t N);
+int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, const std::vector<int64_t> &doff,
+                    const std::vector<int32_t> &files);
+void longfft_free(bpmx_ctx *ctx);
 int bluestein_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, const std::vector<int64_t> &doff,
                       const int64_t *d_doff, const std::vector<int32_t> &files);
 }

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -1866,7 +1867,9 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             const nm_i16 *init = (const nm_i16 *)(mt + 8);
             const nm_i4 *af = (const nm_i4 *)(mt + 8 + 2 * 64 * 16 / 2);
             /* persistent: one 4-wave workgroup per CU (LDS-bound) */
-            const unsigned g1 = (unsigned)std::min<int64_t>((nt + NM_WAVES - 1) / NM_WAVES, 256 * (2 / NM_SLOTS));
+            unsigned g1 = (unsigned)std::min<int64_t>((nt + NM_WAVES - 1) / NM_WAVES, 256 * (2 / NM_SLOTS));
+            if (const char *gv = std::getenv("BPMX_NM_GRID"))    /* diagnostic: fewer persistent workgroups */
+                g1 = std::max(1u, std::min(g1, (unsigned)std::atoi(gv)));
             if (mfma_ks == 3)
                 LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma<3>, dim3(g1), dim3(64 * NM_WAVES), 0, s, a, af,
                        init, mt);
@@ -2021,6 +2024,16 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         }
         f0 = f1;
     }
+    /* long recordings: exact-length four-step DFTs (k_longfft.hip) for every
+     * length that factors for them, rocFFT Bluestein for the rest (or all of
+     * them with BPMX_OPT_HILBERT_BLUESTEIN) */
+    std::vector<int32_t> lf;
+    if (!(P->options & BPMX_OPT_HILBERT_BLUESTEIN)) {
+        std::vector<int32_t> rest;
+        for (int32_t f : blu) (longfft_supported(doff[f + 1] - doff[f]) ? lf : rest).push_back(f);
+        blu.swap(rest);
+    }
+    if ((rc = longfft_hilbert(ctx, s, yd, hb, doff, lf)) != BPMX_OK) return rc;
     if ((rc = bluestein_hilbert(ctx, s, yd, hb, doff, d_doff, blu)) != BPMX_OK) return rc;
     for (int i = 0; i < bpmx_ctx::NSIDE; ++i)       /* join the side streams back into s */
         if (side_used[i]) {

@@ -63,12 +63,18 @@ __device__ __forceinline__ double frame_at(const void *__restrict__ pcm, int ch,
 struct Df2t {
     double b0, b1, b2, b3, b4, a1, a2, a3, a4;
     double z0, z1, z2, z3;
-    /* scipy DOUBLE filt loop: y = Z0 + b0*x; Z_k = Z_{k+1} + x*b_{k+1} - y*a_{k+1} */
+    /* scipy DOUBLE filt loop: y = Z0 + b0*x; Z_k = Z_{k+1} + x*b_{k+1} - y*a_{k+1}.
+     * ZB: b1 = b3 = 0 (every butter band-pass of order 2) and a finite input
+     * (integer PCM): x*0 is a zero and z + (+-0) == z, so those two products
+     * and sums are skipped — equal values (at most the sign of an exact zero
+     * differs, inside all-zero stretches; |y| and the envelope are unchanged) */
+    template <bool ZB = false>
     __device__ __forceinline__ double step(double xn) {
         /* the same rounded operations, the x-only ones first: only
          * z0 + b0 x -> y a1 -> (z1 + x b1) - y a1 is on the chain to the next y */
-        const double bx0 = b0 * xn, bx1 = xn * b1, bx2 = xn * b2, bx3 = xn * b3, bx4 = xn * b4;
-        const double p1 = z1 + bx1, p2 = z2 + bx2, p3 = z3 + bx3;
+        const double bx0 = b0 * xn, bx2 = xn * b2, bx4 = xn * b4;
+        const double bx1 = ZB ? 0.0 : xn * b1, bx3 = ZB ? 0.0 : xn * b3;
+        const double p1 = ZB ? z1 : z1 + bx1, p2 = z2 + bx2, p3 = ZB ? z3 : z3 + bx3;
         const double yn = z0 + bx0;
         z0 = p1 - yn * a1;
         z1 = p2 - yn * a2;
@@ -204,7 +210,96 @@ __global__ __launch_bounds__(256) void k_ref_pick(EnvRefArgs A) {
     }
 }
 
-template <int DT, bool MULTI>
+/* The rolling mean's Kahan add/remove recursion on sum_x alone (chain mode),
+ * storing the running sum of every step as pair rows [i / 2][file][2]: one
+ * 16-B store per two steps (tools/lanebench: 161 -> 87 cycles per step with
+ * the remove stream below).  The value removed at step i is the one added at
+ * step i - w, so for the usual windows (w = sr // 10 = 30..32, W > 0) it
+ * comes from the add stream's registers of this block or the previous one
+ * instead of a second load stream; W = 0 loads it (any window). */
+template <int W>
+__device__ __forceinline__ void kahan_chain(RollMean &R, const double *__restrict__ y, double *__restrict__ ps,
+                                            int64_t S, int64_t off, int64_t w, int64_t nd, int64_t ndmax,
+                                            int64_t ndmin, bool run, int64_t last) {
+    static_assert(W <= PF, "the remove value must lie within the previous block");
+    auto ldy = [&](int64_t i) -> double {
+        i = i < 0 ? 0 : (i > last ? last : i);
+        return fabs(y[i * S]);
+    };
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    auto put = [&](int64_t i, double v) { ps[(i >> 1) * S * 2 + (i & 1)] = v; };
+    const double *pa = y + off * S, *pr = y + (off - w) * S;   /* rows i0 + off, i0 + off - w */
+    const int64_t SP = (int64_t)PF * S;
+    double ca[PF], na[PF], cp[PF], cr[W == 0 ? PF : 1], nr[W == 0 ? PF : 1];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        ca[u] = ldy(u + off);
+        cp[u] = ldy(u + off - PF);
+        if (W == 0) cr[u] = ldy(u + off - w);
+    }
+    for (int64_t i0 = 0; i0 < ndmax; i0 += PF, ps += SP, pa += SP, pr += SP) {
+        if (i0 + PF + off - w >= 0 && i0 + 2 * PF + off <= ndmin) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                na[u] = fabs(pa[SP + u * S]);
+                if (W == 0) nr[u] = fabs(pr[SP + u * S]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int64_t i = i0 + PF + u;
+                na[u] = ldy(i + off);
+                if (W == 0) nr[u] = ldy(i + off - w);
+            }
+        }
+        /* removed value of step i0 + u: |y[i0 + u + off - w]| */
+        auto rem = [&](int u) -> double {
+            if (W == 0) return cr[u];
+            return u >= W ? ca[u - W] : cp[u - W + PF];
+        };
+        if (i0 >= w - off && i0 + PF + off <= ndmin) {
+            /* steady state, no NaN in the wave: pandas remove_mean / add_mean's sum_x updates */
+            double sum = R.sum, cad = R.cadd, crm = R.crem;
+            double sv[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const double yr = -rem(u) - crm, tr = sum + yr;
+                crm = (tr - sum) - yr;
+                sum = tr;
+                const double ya = ca[u] - cad, ta = sum + ya;
+                cad = (ta - sum) - ya;
+                sum = ta;
+                sv[u] = sum;
+            }
+            if (run) {
+#pragma unroll
+                for (int u = 0; u < PF; u += 2) *(dv2 *)(ps + (u >> 1) * S * 2) = dv2{sv[u], sv[u + 1]};
+            }
+            R.sum = sum; R.cadd = cad; R.crem = crm;
+        } else {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int64_t i = i0 + u;
+                if (run && i < nd) {
+                    if (i > 0) {
+                        const int64_t s = i + 1 + off - w;
+                        if (s > 0 && s <= nd) R.remove(rem(u));
+                        if (i + off < nd) R.add(ca[u]);
+                    }
+                    put(u, R.sum);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            cp[u] = ca[u];
+            ca[u] = na[u];
+            if (W == 0) cr[u] = nr[u];
+        }
+    }
+}
+
+template <int DT, bool MULTI, bool ZB>
 __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     __shared__ double st_env[STG][65];
     __shared__ double st_y[STG][65];
@@ -263,12 +358,12 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
             if (r0 + PFB <= nemin) {
                 if (run) {
 #pragma unroll
-                    for (int u = 0; u < PFB; ++u) p[u * S] = D.step(cur[u]);
+                    for (int u = 0; u < PFB; ++u) p[u * S] = D.step<ZB>(cur[u]);
                 }
             } else if (run) {
 #pragma unroll
                 for (int u = 0; u < PFB; ++u)
-                    if (r0 + u < ne) p[u * S] = D.step(cur[u]);
+                    if (r0 + u < ne) p[u * S] = D.step<ZB>(cur[u]);
             }
 #pragma unroll
             for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
@@ -301,7 +396,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
                 if (run) {
 #pragma unroll
                     for (int u = 0; u < PFB; ++u) {
-                        const double yv = D.step(cur[u]);
+                        const double yv = D.step<ZB>(cur[u]);
                         nanseen |= yv != yv;
                         p[-u * S] = yv;
                     }
@@ -310,7 +405,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
 #pragma unroll
                 for (int u = 0; u < PFB; ++u)
                     if (r0 + u < ne) {
-                        const double yv = D.step(cur[u]);
+                        const double yv = D.step<ZB>(cur[u]);
                         nanseen |= yv != yv;
                         p[-u * S] = yv;
                     }
@@ -342,54 +437,12 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         if (have && A.chain) A.chain[f] = chain && run ? 1 : 0;
         if (chain) {
             /* only the Kahan recursion; k_ref_env_mean forms the means */
-            double *__restrict__ ps = A.sums + (have ? f : 0);          /* row i0 of the running sums */
-            const double *pa = y + off * S, *pr = y + (off - w) * S;   /* rows i0 + off, i0 + off - w */
-            const int64_t SP = (int64_t)PF * S;
-            double ca[PF], cr[PF], na[PF], nr[PF];
-#pragma unroll
-            for (int u = 0; u < PF; ++u) { ca[u] = ldy(u + off); cr[u] = ldy(u + off - w); }
-            for (int64_t i0 = 0; i0 < ndmax; i0 += PF, ps += SP, pa += SP, pr += SP) {
-                if (i0 + PF + off - w >= 0 && i0 + 2 * PF + off <= ndmin) {
-#pragma unroll
-                    for (int u = 0; u < PF; ++u) { na[u] = fabs(pa[SP + u * S]); nr[u] = fabs(pr[SP + u * S]); }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < PF; ++u) {
-                        const int64_t i = i0 + PF + u;
-                        na[u] = ldy(i + off);
-                        nr[u] = ldy(i + off - w);
-                    }
-                }
-                if (i0 >= w - off && i0 + PF + off <= ndmin) {
-                    /* steady state, no NaN in the wave: pandas remove_mean / add_mean's sum_x updates */
-                    double sum = R.sum, cad = R.cadd, crm = R.crem;
-#pragma unroll
-                    for (int u = 0; u < PF; ++u) {
-                        const double yr = -cr[u] - crm, tr = sum + yr;
-                        crm = (tr - sum) - yr;
-                        sum = tr;
-                        const double ya = ca[u] - cad, ta = sum + ya;
-                        cad = (ta - sum) - ya;
-                        sum = ta;
-                        if (run) ps[u * S] = sum;
-                    }
-                    R.sum = sum; R.cadd = cad; R.crem = crm;
-                } else {
-#pragma unroll
-                    for (int u = 0; u < PF; ++u) {
-                        const int64_t i = i0 + u;
-                        if (run && i < nd) {
-                            if (i > 0) {
-                                const int64_t s = i + 1 + off - w;
-                                if (s > 0 && s <= nd) R.remove(cr[u]);
-                                if (i + off < nd) R.add(ca[u]);
-                            }
-                            ps[u * S] = R.sum;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < PF; ++u) { ca[u] = na[u]; cr[u] = nr[u]; }
+            double *__restrict__ ps = A.sums + (have ? (int64_t)f * 2 : 0);   /* pair rows [i / 2][file][2] */
+            switch (w) {
+            case 30: kahan_chain<30>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
+            case 31: kahan_chain<31>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
+            case 32: kahan_chain<32>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
+            default: kahan_chain<0>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
             }
             STAMP(2);
             STAMP_FLUSH(A.stamps);
@@ -473,7 +526,7 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
     const int64_t i00 = (int64_t)blockIdx.x * STG;
     if (!__syncthreads_or(mine && i00 < nd)) return;
     const double *__restrict__ y = A.scratch + 15 * S + (have ? f : 0);
-    const double *__restrict__ sums = A.sums + (have ? f : 0);
+    const double *__restrict__ sums = A.sums + (have ? (int64_t)f * 2 : 0);     /* pair rows [i / 2][file][2] */
     /* this wave's 16 rows: every load issued first, then the arithmetic */
     constexpr int R = STG / 4;
     const int64_t ib = i00 + wv * R;
@@ -485,7 +538,7 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
         const bool ok = mine && i < nd;
         const int64_t ic = ok ? i : 0;
         const int64_t a = ic + off < lastr ? ic + off : lastr;            /* last added index */
-        sm[r] = ok ? sums[ic * S] : 0.0;
+        sm[r] = ok ? sums[(ic >> 1) * S * 2 + (ic & 1)] : 0.0;
         ya[r] = ok ? y[a * S] : 0.0;
         yb[r] = ok && a > 0 ? y[(a - 1) * S] : 0.0;
         yi[r] = ok ? y[ic * S] : 0.0;
@@ -535,15 +588,21 @@ template __global__ void k_ref_pick<BPMX_DT_I16, true>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_I32, true>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_F32, true>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_F64, true>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_U8, false>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_I16, false>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_I32, false>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_F32, false>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_F64, false>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_U8, true>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_I16, true>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_I32, true>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_F32, true>(EnvRefArgs);
-template __global__ void k_envelope_ref_t<BPMX_DT_F64, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, false, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, true, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, false, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, true, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, false, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, true, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F32, false, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F32, true, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F64, false, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_F64, true, false>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, false, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_U8, true, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, false, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I16, true, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, false, true>(EnvRefArgs);
+template __global__ void k_envelope_ref_t<BPMX_DT_I32, true, true>(EnvRefArgs);
 
 }  // namespace bpmx

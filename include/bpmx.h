@@ -95,7 +95,9 @@ enum bpmx_option {
                                     transform (test/diagnostic) */
     BPMX_OPT_REF_SERIAL_MEAN = 1024, /* reference mode: form the rolling mean's outputs inside the sequential
                                         pass instead of from its running sums in parallel (test/diagnostic) */
-    BPMX_OPT_STATS = 2048            /* count the run's path decisions for bpmx_stats (diagnostic) */
+    BPMX_OPT_STATS = 2048,           /* count the run's path decisions for bpmx_stats (diagnostic) */
+    BPMX_OPT_HILBERT_BLUESTEIN = 4096 /* native mode, long recordings: rocFFT Bluestein instead of the exact-
+                                         length four-step transform (test/diagnostic) */
 };
 
 /* bpmx_stats counters of the last run with BPMX_OPT_STATS */

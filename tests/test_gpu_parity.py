@@ -985,3 +985,28 @@ def test_config_c5_shard_of_eight(det):
         _check_file(host[k], o, exact_env=False)
     for h, n in zip(host, lens):
         assert len(h["env"]) == -(-int(n) // 300) and len(h["peaks"]) > 10 * (n // fs // 60)
+
+
+def test_longfft_hilbert_matches_bluestein_and_oracle(det):
+    """Long recordings' Hilbert transform by exact-length four-step DFTs
+    (k_longfft.hip) against the rocFFT Bluestein path (BPMX_OPT_HILBERT_BLUESTEIN)
+    and the oracle: lengths with a large prime row (s = 601, 1201: Bluestein
+    rows inside the workgroup; s = 1742 = 2 x 13 x 67: 4160-point rows), a
+    smooth one (s = 1800) and an odd Nd (unpacked transform), 96 kHz mono."""
+    import torch
+    from bpm_analysis_amd import _native as N
+    fs = 96000
+    lens = [96000 * 601, 96000 * 1742 // 2, 300 * 95_993, 96000 * 1200 // 2]
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    pcm = det.synth(fo, fs, 1, seed0=321)
+    params = dict(G.BASE_PARAMS)
+    a = det.run(pcm, fo, fs, params, mode="native").to_host()
+    b = det.run(pcm, fo, fs, params, mode="native", options=N.OPT_HILBERT_BLUESTEIN).to_host()
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        scale = np.max(np.abs(y["env"]))
+        assert np.max(np.abs(x["env"] - y["env"])) <= 1e-12 * scale
+        assert _same(x["peaks"], y["peaks"]) and _same(x["troughs"], y["troughs"])
+    o = O.detect(O.synth(321 + 2, lens[2], fs, 1), fs, params, mode="native")     # odd Nd = 95,993 = 59 x 1627
+    assert len(a[2]["env"]) == 95_993
+    _check_file(a[2], o, exact_env=False)

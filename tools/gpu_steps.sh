@@ -34,6 +34,8 @@ for step in "$@"; do
     pipesweep_ref) run pipesweep_ref 600 python tools/pipe_sweep.py --steps 5 --mode reference --shapes 0,0,0 4,0,0 4,192,0 0,0,0 ;;
     fpref) run dump_env_ref 300 python tools/dump_env.py 1024 reference /tmp/env_ref.bin && run fpbench_ref 120 ./tools/fpbench /tmp/env_ref.bin l ;;
     fpnat) run dump_env_nat 300 python tools/dump_env.py 1024 native /tmp/env_nat.bin && run fpbench_nat 120 ./tools/fpbench /tmp/env_nat.bin l ;;
+    pipesweep_word) BPMX_CUMASK_PER_WORD=1 run pipesweep_word 600 python tools/pipe_sweep.py --steps 10 --shapes 0,0,0 4,192,0 4,224,0 4,192,64 0,0,0 ;;
+    pipesweep_grid) run pipesweep_grid 600 python tools/pipe_sweep.py --steps 10 --shapes 0,0,0,0 0,0,0,448 0,0,0,384 0,0,0,320 2,0,0,384 4,0,0,384 2,0,0,320 4,0,0,320 8,0,0,384 0,0,0,0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

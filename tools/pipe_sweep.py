@@ -45,7 +45,12 @@ def main():
     ref = None
     rows = []
     for sh in a.shapes:
-        k, ec, dc = (int(x) for x in sh.split(","))
+        parts = [int(x) for x in sh.split(",")]
+        k, ec, dc = parts[:3]
+        if len(parts) > 3 and parts[3] > 0:           # persistent grid of the block kernel (BPMX_NM_GRID)
+            os.environ["BPMX_NM_GRID"] = str(parts[3])
+        else:
+            os.environ.pop("BPMX_NM_GRID", None)
         det.set_pipeline(k, ec, dc)
         for _ in range(2):
             det.run(pcm, fo, fs, params, mode=a.mode, out=out, d=d, options=a.options)
@@ -61,7 +66,8 @@ def main():
             ref = cur
         same = all(np.array_equal(x, y, equal_nan=True) if isinstance(x, np.ndarray) else x == y
                    for kk in cur for x, y in zip(cur[kk], ref[kk]))
-        row = {"chunks": k, "env_cus": ec, "det_cus": dc, "ms_per_step": round(ms, 4), "identical": bool(same)}
+        row = {"chunks": k, "env_cus": ec, "det_cus": dc, "nm_grid": parts[3] if len(parts) > 3 else 0,
+               "ms_per_step": round(ms, 4), "identical": bool(same)}
         rows.append(row)
         print(json.dumps(row), flush=True)
     det.set_pipeline(0, 0, 0)
