@@ -486,7 +486,17 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.skip = nullptr;
         a.stats = 0;                      /* k_find_peaks builds its own block tables when it runs */
         LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-        if (long_files && (rc = quantile_long(a)) != BPMX_OK) return rc;
+        if (long_files) {
+            /* long recordings take the noise-floor level in the same passes (one
+             * more compare per key) instead of a second 15-launch round later */
+            QuantArgs al = a;
+            if (noise_lazy) {
+                al.q[al.n_levels] = P->noise_floor_q;
+                al.slot[al.n_levels] = 1 << Q_NOISE;
+                al.n_levels++;
+            }
+            if ((rc = quantile_long(al)) != BPMX_OK) return rc;
+        }
     }
 
     /* ---- FLOOR ---- */
@@ -512,7 +522,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.n_levels = 1; a.q[0] = P->noise_floor_q; a.slot[0] = 1 << Q_NOISE;
             a.skip = d_run1; a.stats = 0;
             LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
-            if (long_files && (rc = quantile_long(a)) != BPMX_OK) return rc;
+            /* long recordings computed this level with the others (at most three
+             * distinct levels before it, so it always fits in Q_SLOTS) */
         }
         /* rolling-quantile geometry: T outputs per step, sorted union in LDS */
         const int64_t W = bad_window ? P->min_periods : P->noise_window;
@@ -660,6 +671,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.dec = tdec; a.exact = d_exact;
             a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
             a.stats = d_stats;
+            a.lu = (double2 *)ctx->buf("trough_lu", (size_t)sumnd * 16, &rc);
+            if (rc != BPMX_OK) return rc;
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
             const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);

@@ -25,8 +25,8 @@
  * A row DFT is a Stockham autosort over mixed radices (2..64) with the n-th
  * roots of unity tabulated in LDS, or, for a prime n > 64 (the large prime
  * factor of a ragged length), Bluestein's chirp-z inside the workgroup: a
- * power-of-two cyclic convolution of length L >= 2n - 1 <= 4096 against
- * FFT_L(b), tabulated once per prime.  M's largest prime factor p > 64 takes
+ * cyclic convolution of length L >= 2n - 1 (L <= 4096) against
+ * FFT_L(b), tabulated once per prime (L the shortest 2^a 3^b 5^c >= 2n - 1).  M's largest prime factor p > 64 takes
  * A = p (p <= 2047) and B = M / p; a smooth M splits near its square root.
  * Rows are at most LF_NMAX points.  Anything else stays on the rocFFT path.
  */
@@ -52,17 +52,29 @@ constexpr int LF_TS = 32;          /* transpose tile */
 struct LfSub {                     /* an n-point DFT in LDS */
     int32_t n, L, nrad, rpw;       /* L > 0: Bluestein for prime n over L points; rows per workgroup */
     int32_t rad[LF_MAXR];          /* Stockham radices of n (or of L) */
-    int64_t fb;                    /* Bluestein: FFT_L(b) at table + fb */
+    int64_t fb;                    /* Bluestein: FFT_L(b) at fbt + fb */
+    int64_t toff;                  /* tab: roots e^(-2 pi i t / n) (direct) or chirp c_m (Bluestein) */
+    int64_t loff;                  /* Bluestein / Rader: tab offset of the roots of L */
+    int32_t kind, pad2;            /* 0 direct, 1 Bluestein, 2 Rader (L = n - 1) */
+    int64_t ioff;                  /* Rader: itab + ioff: g^q mod n, then g^-q mod n (q < n - 1) */
 };
 struct LfRec {                     /* one recording */
     int64_t d0, w0;                /* decimated offset (y, h); work offset (double2) */
-    int32_t N, M, A, B, pack, sa, sb, pad;
+    int64_t toff;                  /* tab: w_M^t for t < T, then w_M^(u T) for u < ceil(M / T) */
+    int32_t N, M, A, B, pack, sa, sb, twT;
+};
+/* table fill descriptors (once per geometry) */
+struct LfTab {
+    int64_t off;
+    int32_t count, kind, n, T;     /* kind 0: e^(-2 pi i t / n); 1: e^(-i pi t^2 / n); 2: e^(-2 pi i (t T mod n) / n) */
 };
 struct LfArgs {
     const double *yd;
     double *hb;
     double2 *w1, *w2;
     const double2 *fbt;            /* FFT_L(b) tables */
+    const double2 *tab;            /* roots, chirps, four-step twiddles */
+    const int32_t *itab;           /* Rader permutations */
     const LfRec *rec;
     const LfSub *sub;
     const int32_t *pre;            /* work-item prefix over the recordings [R + 1] */
@@ -88,6 +100,13 @@ __device__ __forceinline__ int rec_of(const int32_t *pre, int R, int g) {
     int lo = 0, hi = R;
     while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (pre[mid] <= g) lo = mid; else hi = mid; }
     return lo;
+}
+
+/* w_M^t = e^(-2 pi i t / M) from the recording's two-level table (sign +1: conjugate) */
+__device__ __forceinline__ double2 twid(const double2 *tab, const LfRec &rc, int64_t t, int sign) {
+    const uint32_t hi = (uint32_t)t / (uint32_t)rc.twT, lo = (uint32_t)t - hi * (uint32_t)rc.twT;
+    const double2 w = cmul(tab[rc.toff + lo], tab[rc.toff + rc.twT + hi]);
+    return sign < 0 ? w : conj2(w);
 }
 
 /* x / d for 0 <= x < 2^22 (a float reciprocal, then one correction) */
@@ -147,6 +166,32 @@ __device__ __forceinline__ void lf_stage(double2 *x, const double2 *rt, int n, i
                 o[2] = sub2(s02, s13);
                 o[1] = add2(d02, wd);
                 o[3] = sub2(d02, wd);
+            } else if (R == 8) {
+                /* radix 2 x 4: a_k = v_k + v_(k+4), b_k = (v_k - v_(k+4)) w8^k, then two
+                 * 4-point DFTs give the even and the odd outputs; w8 = e^(sign i pi / 4) */
+                const double2 w4 = rt[2 * nR];                  /* w8^2 = sign * i */
+                const double sg = w4.y, h = 0.70710678118654752440;
+                double2 a[4], bb[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a[k] = add2(v[it][k], v[it][k + 4]);
+                    bb[k] = sub2(v[it][k], v[it][k + 4]);
+                }
+                /* b1 *= (1 + sg i) / sqrt 2, b2 *= sg i, b3 *= (-1 + sg i) / sqrt 2 */
+                bb[1] = make_double2(h * (bb[1].x - sg * bb[1].y), h * (bb[1].y + sg * bb[1].x));
+                bb[2] = make_double2(-sg * bb[2].y, sg * bb[2].x);
+                bb[3] = make_double2(h * (-bb[3].x - sg * bb[3].y), h * (-bb[3].y + sg * bb[3].x));
+                auto dft4 = [&](const double2 *x4, double2 *y0, double2 *y1, double2 *y2, double2 *y3) {
+                    const double2 s02 = add2(x4[0], x4[2]), d02 = sub2(x4[0], x4[2]);
+                    const double2 s13 = add2(x4[1], x4[3]), d13 = sub2(x4[1], x4[3]);
+                    const double2 wd = make_double2(-sg * d13.y, sg * d13.x);
+                    *y0 = add2(s02, s13);
+                    *y2 = sub2(s02, s13);
+                    *y1 = add2(d02, wd);
+                    *y3 = sub2(d02, wd);
+                };
+                dft4(a, &o[0], &o[2], &o[4], &o[6]);
+                dft4(bb, &o[1], &o[3], &o[5], &o[7]);
             } else {
 #pragma unroll
                 for (int k = 0; k < R; ++k) {
@@ -222,6 +267,7 @@ __device__ __forceinline__ void lds_fft(double2 *x, const double2 *rt, int n, in
         case 3: lf_stage<3>(x, rt, n, nrows, Ns); break;
         case 4: lf_stage<4>(x, rt, n, nrows, Ns); break;
         case 5: lf_stage<5>(x, rt, n, nrows, Ns); break;
+        case 8: lf_stage<8>(x, rt, n, nrows, Ns); break;
         default: lf_stage_gen(x, rt, n, nrows, Ns, R); break;
         }
         Ns *= R;
@@ -294,17 +340,78 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
     if (Lb == 0) {
         double2 *x = lds, *rt = lds + (int64_t)rpw * n;
         for (int i = tid; i < nr * n; i += LF_T) x[i] = row0[i];
-        for (int i = tid; i < n; i += LF_T) rt[i] = root(i, n, sign);
+        for (int i = tid; i < n; i += LF_T) {
+            const double2 w = A.tab[sbp->toff + i];
+            rt[i] = sign < 0 ? w : conj2(w);
+        }
         __syncthreads();
         lds_fft(x, rt, n, nr, sbp->rad, nrad);
-        const float rn = 1.0f / (float)n;
-        for (int i = tid; i < nr * n; i += LF_T) {
-            double2 v = x[i];
-            if (tw) {
-                const int qq = fdiv(i, n, rn), k = i - qq * n;
-                v = cmul(v, root(((int64_t)(q0 + qq) * k) % M, M, sign));
+        if (!tw) {
+            for (int i = tid; i < nr * n; i += LF_T) row0[i] = x[i];
+            return;
+        }
+        /* element k of row q times w_M^(q k): t = q k mod M stepped by q LF_T */
+        for (int qq = 0; qq < nr; ++qq) {
+            const int64_t q = q0 + qq, d = (q * LF_T) % M;
+            int64_t t = (q * tid) % M;
+            for (int k = tid; k < n; k += LF_T) {
+                row0[(int64_t)qq * n + k] = cmul(x[qq * n + k], twid(A.tab, rc, t, sign));
+                t += d;
+                if (t >= M) t -= M;
             }
-            row0[i] = v;
+        }
+        return;
+    }
+    if (sbp->kind == 2) {
+        /* Rader, prime n with a smooth n - 1 = P (rpw rows per workgroup): with
+         * g a primitive root, a_q = x_(g^q), b_q = w_n^(g^-q) (w_n =
+         * e^(-2 pi i / n); the inverse transform conjugates), X_(g^-m) = x_0 +
+         * (a (*) b)_m, the cyclic convolution by FFT_P; X_0 = x_0 + sum_q a_q =
+         * x_0 + FFT_P(a)_0 */
+        const int P = Lb;
+        double2 *xin = lds, *a = lds + (int64_t)rpw * n, *rt = a + (int64_t)rpw * P;
+        __shared__ double2 s_x0[64], s_X0[64];
+        const int32_t *perm = A.itab + sbp->ioff, *iperm = perm + P;
+        for (int i = tid; i < nr * n; i += LF_T) xin[i] = row0[i];
+        for (int i = tid; i < P; i += LF_T) rt[i] = A.tab[sbp->loff + i];
+        __syncthreads();
+        const float rP = 1.0f / (float)P, rn = 1.0f / (float)n;
+        for (int i = tid; i < nr * P; i += LF_T) {
+            const int r = fdiv(i, P, rP), q = i - r * P;
+            a[i] = xin[r * n + perm[q]];
+        }
+        __syncthreads();
+        lds_fft(a, rt, P, nr, sbp->rad, nrad);
+        for (int r = tid; r < nr; r += LF_T) {
+            s_x0[r] = xin[r * n];
+            s_X0[r] = add2(xin[r * n], a[r * P]);
+        }
+        __syncthreads();
+        const double2 *fb = A.fbt + sbp->fb + (sign < 0 ? 0 : P);
+        for (int i = tid; i < nr * P; i += LF_T) a[i] = cmul(a[i], fb[i - fdiv(i, P, rP) * P]);
+        for (int i = tid; i < P; i += LF_T) rt[i] = conj2(rt[i]);
+        __syncthreads();
+        lds_fft(a, rt, P, nr, sbp->rad, nrad);
+        /* unpermute into LDS (x_0 is saved), then one coalesced pass with the
+         * four-step twiddle */
+        const double invP = 1.0 / (double)P;
+        for (int i = tid; i < nr * n; i += LF_T) {
+            const int r = fdiv(i, n, rn), m = i - r * n;     /* m = P stands for X_0 */
+            xin[r * n + (m == P ? 0 : iperm[m])] = m == P ? s_X0[r] : add2(s_x0[r], scale2(a[r * P + m], invP));
+        }
+        __syncthreads();
+        if (!tw) {
+            for (int i = tid; i < nr * n; i += LF_T) row0[i] = xin[i];
+            return;
+        }
+        for (int qq = 0; qq < nr; ++qq) {
+            const int64_t q = q0 + qq, d = (q * LF_T) % M;
+            int64_t t = (q * tid) % M;
+            for (int k = tid; k < n; k += LF_T) {
+                row0[(int64_t)qq * n + k] = cmul(xin[qq * n + k], twid(A.tab, rc, t, sign));
+                t += d;
+                if (t >= M) t -= M;
+            }
         }
         return;
     }
@@ -314,15 +421,11 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
      * or its conjugate */
     const int L = Lb;
     double2 *x = lds, *rt = lds + L;
-    auto chirp = [&](int64_t m) -> double2 {
-        const int64_t e = (m * m) % (2 * (int64_t)n);
-        double sn, cs;
-        sincospi((double)e / (double)n, &sn, &cs);
-        return make_double2(cs, sign < 0 ? -sn : sn);
-    };
+    const double2 *ch = A.tab + sbp->toff;                  /* c_m = e^(-i pi m^2 / n) */
+    auto chirp = [&](int m) -> double2 { const double2 c = ch[m]; return sign < 0 ? c : conj2(c); };
     for (int i = tid; i < L; i += LF_T) {
         x[i] = i < n ? cmul(row0[i], chirp(i)) : make_double2(0.0, 0.0);
-        rt[i] = root(i, L, -1);
+        rt[i] = A.tab[sbp->loff + i];
     }
     __syncthreads();
     lds_fft(x, rt, L, 1, sbp->rad, nrad);
@@ -335,35 +438,70 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
     __syncthreads();
     lds_fft(x, rt, L, 1, sbp->rad, nrad);
     const double invL = 1.0 / (double)L;
+    const int64_t d = ((int64_t)q0 * LF_T) % M;
+    int64_t t = ((int64_t)q0 * tid) % M;
     for (int i = tid; i < n; i += LF_T) {
         double2 v = scale2(cmul(x[i], chirp(i)), invL);
-        if (tw) v = cmul(v, root(((int64_t)q0 * i) % M, M, sign));
+        if (tw) v = cmul(v, twid(A.tab, rc, t, sign));
         row0[i] = v;
+        t += d;
+        if (t >= M) t -= M;
     }
 }
 
 /* FFT_L(b) of one Bluestein prime: b_m = conj(c_m) for m < n, b_(L-m) =
  * conj(c_m) for 0 < m < n, else 0 (one workgroup per prime) */
-__global__ __launch_bounds__(LF_T) void k_lf_blu_b(const LfSub *sub, const int32_t *which, double2 *fbt) {
+__global__ __launch_bounds__(LF_T) void k_lf_blu_b(const LfSub *sub, const int32_t *which, const double2 *tab,
+                                                  double2 *fbt) {
     extern __shared__ double2 lds[];
     const LfSub *sbp = sub + which[blockIdx.x];
     const int n = sbp->n, L = sbp->L, tid = threadIdx.x;
     double2 *x = lds, *rt = lds + L;
     for (int i = tid; i < L; i += LF_T) {
         const int m = i < n ? i : (i > L - n ? L - i : -1);
-        double2 v = make_double2(0.0, 0.0);
-        if (m >= 0) {
-            const int64_t e = ((int64_t)m * m) % (2 * (int64_t)n);
-            double sn, cs;
-            sincospi((double)e / (double)n, &sn, &cs);
-            v = make_double2(cs, sn);                      /* conj(c_m) */
-        }
-        x[i] = v;
-        rt[i] = root(i, L, -1);
+        x[i] = m >= 0 ? conj2(tab[sbp->toff + m]) : make_double2(0.0, 0.0);
+        rt[i] = tab[sbp->loff + i];
     }
     __syncthreads();
     lds_fft(x, rt, L, 1, sbp->rad, sbp->nrad);
     for (int i = tid; i < L; i += LF_T) fbt[sbp->fb + i] = x[i];
+}
+
+/* FFT_P(b) and FFT_P(conj b) of one Rader prime, b_q = w_n^(g^-q) */
+__global__ __launch_bounds__(LF_T) void k_lf_rader_b(const LfSub *sub, const int32_t *which, const double2 *tab,
+                                                    const int32_t *itab, double2 *fbt) {
+    extern __shared__ double2 lds[];
+    const LfSub *sbp = sub + which[blockIdx.x];
+    const int P = sbp->L, tid = threadIdx.x;
+    const int32_t *iperm = itab + sbp->ioff + P;
+    double2 *x = lds, *rt = lds + P;
+    for (int c = 0; c < 2; ++c) {
+        for (int i = tid; i < P; i += LF_T) {
+            const double2 b = tab[sbp->toff + iperm[i]];
+            x[i] = c == 0 ? b : conj2(b);
+            rt[i] = tab[sbp->loff + i];
+        }
+        __syncthreads();
+        lds_fft(x, rt, P, 1, sbp->rad, sbp->nrad);
+        for (int i = tid; i < P; i += LF_T) fbt[sbp->fb + c * P + i] = x[i];
+        __syncthreads();
+    }
+}
+
+/* the tables: one workgroup row per descriptor, exact arguments for sincospi */
+__global__ __launch_bounds__(256) void k_lf_tab(const LfTab *desc, double2 *tab) {
+    const LfTab d = desc[blockIdx.y];
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= d.count) return;
+    double sn, cs;
+    if (d.kind == 1) {
+        const int64_t e = (t * t) % (2 * (int64_t)d.n);
+        sincospi((double)e / (double)d.n, &sn, &cs);
+    } else {
+        const int64_t e = d.kind == 2 ? (t * d.T) % d.n : t;
+        sincospi(2.0 * (double)e / (double)d.n, &sn, &cs);
+    }
+    tab[d.off + t] = make_double2(cs, -sn);
 }
 
 /* forward DFT Z at [k mod A][k div A]: real-FFT split, Hilbert multiplier,
@@ -430,10 +568,27 @@ bool radices(int64_t n, std::vector<int> &out) {
         if (p > LF_RMAX) return false;
         if (p == 2) ++twos; else odd.push_back(p);
     }
-    for (; twos >= 2; twos -= 2) out.push_back(4);
-    if (twos) out.push_back(2);
+    for (; twos >= 3; twos -= 3) out.push_back(8);
+    if (twos == 2) out.push_back(4);
+    if (twos == 1) out.push_back(2);
     for (int p : odd) out.push_back(p);
     return (int)out.size() <= LF_MAXR;
+}
+/* the least primitive root of a prime p, or 0 */
+int32_t primitive_root(int64_t p) {
+    if (p < 3) return 0;
+    std::vector<int> f = factorize(p - 1);
+    f.erase(std::unique(f.begin(), f.end()), f.end());
+    for (int64_t g = 2; g < p; ++g) {
+        bool ok = true;
+        for (int q : f) {
+            int64_t e = (p - 1) / q, r = 1, b = g;
+            while (e) { if (e & 1) r = r * b % p; b = b * b % p; e >>= 1; }
+            if (r == 1) { ok = false; break; }
+        }
+        if (ok) return (int32_t)g;
+    }
+    return 0;
 }
 }  // namespace
 
@@ -443,8 +598,9 @@ struct LfHost {
     std::vector<int64_t> key;
     std::vector<LfRec> recs;
     std::vector<LfSub> subs;
-    std::vector<int32_t> pre, blu;
-    int64_t fbsz = 0, work = 0;
+    std::vector<int32_t> pre, blu, rad, itab;
+    std::vector<LfTab> tabs;
+    int64_t fbsz = 0, work = 0, tabsz = 0;
     size_t lds = 0;
     bool uploaded = false;
 };
@@ -499,23 +655,63 @@ int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, 
         std::vector<LfRec> recs(R);
         std::vector<LfSub> subs;
         std::map<int32_t, int32_t> sub_of;
-        int64_t fbsz = 0;
-        std::vector<int32_t> blu;
+        std::map<int32_t, int64_t> root_of;                  /* Bluestein lengths' root tables */
+        int64_t fbsz = 0, tabsz = 0;
+        std::vector<int32_t> blu, rad, itab;
+        std::vector<LfTab> tabs;
         auto get_sub = [&](int32_t n) -> int32_t {
             auto it = sub_of.find(n);
             if (it != sub_of.end()) return it->second;
             LfSub sb{};
             sb.n = n;
-            std::vector<int> rd;
-            if (radices(n, rd)) {
+            std::vector<int> rd, rp;
+            const bool direct = radices(n, rd);
+            const bool rader = !direct && radices(n - 1, rp) && primitive_root(n) > 0;
+            sb.kind = direct ? 0 : (rader ? 2 : 1);
+            sb.toff = tabsz;
+            tabs.push_back(LfTab{tabsz, n, sb.kind == 1 ? 1 : 0, n, 0});    /* roots of n, or chirps */
+            tabsz += n;
+            auto roots_of = [&](int32_t L) -> int64_t {
+                auto lt = root_of.find(L);
+                if (lt == root_of.end()) {
+                    lt = root_of.emplace(L, tabsz).first;
+                    tabs.push_back(LfTab{tabsz, L, 0, L, 0});
+                    tabsz += L;
+                }
+                return lt->second;
+            };
+            if (direct) {
                 sb.L = 0;
                 sb.rpw = std::max(1, LF_GROUP / n);
+            } else if (rader) {
+                /* g^q and g^-q mod n; the convolution kernels' spectra at fb (forward, inverse) */
+                const int32_t P = n - 1, g = primitive_root(n);
+                /* rows per workgroup: LF_GROUP points, within ~144 KB of LDS */
+                sb.rpw = std::max(1, std::min({LF_GROUP / P, (9216 - P) / (n + P), 64}));
+                sb.L = P;
+                rd = rp;
+                sb.loff = roots_of(P);
+                sb.ioff = (int64_t)itab.size();
+                std::vector<int32_t> pw(P);
+                int64_t v = 1;
+                for (int q = 0; q < P; ++q) { pw[q] = (int32_t)v; v = v * g % n; }
+                for (int q = 0; q < P; ++q) itab.push_back(pw[q]);
+                for (int q = 0; q < P; ++q) itab.push_back(pw[(P - q) % P]);     /* g^-q = g^(P - q) */
+                sb.fb = fbsz;
+                fbsz += 2 * P;
+                rad.push_back((int32_t)subs.size());
             } else {
                 sb.rpw = 1;
-                int32_t L = 1;
-                while (L < 2 * n - 1) L <<= 1;
+                /* the shortest 2^a 3^b 5^c >= 2n - 1 (power-of-two padding would
+                 * cost ~40 % more butterflies over C5's lengths) */
+                int32_t L = 0;
+                for (int64_t p2 = 1; p2 <= LF_LMAX; p2 *= 2)
+                    for (int64_t p3 = p2; p3 <= LF_LMAX; p3 *= 3)
+                        for (int64_t p5 = p3; p5 <= LF_LMAX; p5 *= 5)
+                            if (p5 >= 2 * n - 1 && (L == 0 || p5 < L)) L = (int32_t)p5;
                 sb.L = L;
                 radices(L, rd);
+                sb.loff = roots_of(L);
                 sb.fb = fbsz;
                 fbsz += L;
                 blu.push_back((int32_t)subs.size());
@@ -539,9 +735,16 @@ int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, 
             r.sb = get_sub(r.B);
             r.w0 = w;
             w += r.M;
+            r.twT = (int32_t)std::ceil(std::sqrt((double)r.M));
+            const int32_t nhi = (r.M + r.twT - 1) / r.twT;
+            r.toff = tabsz;
+            tabs.push_back(LfTab{tabsz, r.twT, 0, r.M, 0});
+            tabs.push_back(LfTab{tabsz + r.twT, nhi, 2, r.M, r.twT});
+            tabsz += r.twT + nhi;
         }
         for (auto &sb : subs)
-            lds = std::max(lds, (size_t)(sb.L ? 2 * sb.L : (sb.rpw + 1) * sb.n) * sizeof(double2));
+            lds = std::max(lds, (size_t)(sb.kind == 0 ? (sb.rpw + 1) * sb.n
+                                         : sb.kind == 1 ? 2 * sb.L : sb.rpw * (sb.n + sb.L) + sb.L) * sizeof(double2));
         /* prefixes: tiles (T1, T1' over [A][B] / [B][A]: same count), rows of B
          * (R1, R1': B rows of A points), rows of A (R2, R2'), mid groups */
         std::vector<int32_t> pre(4 * (R + 1), 0);
@@ -558,16 +761,25 @@ int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, 
         H.subs = subs;
         H.pre = pre;
         H.blu = blu;
+        H.rad = rad;
+        H.itab = itab;
         H.fbsz = fbsz;
+        H.tabs = tabs;
+        H.tabsz = tabsz;
         H.work = w;
         H.lds = lds;
         H.key = key;
         H.uploaded = false;
     }
     const size_t nrec = H.recs.size() * sizeof(LfRec), nsub = H.subs.size() * sizeof(LfSub);
-    const size_t npre = H.pre.size() * 4, nblu = std::max<size_t>(1, H.blu.size()) * 4;
-    bool grew_m = false, grew_w = false, grew_b = false;
-    char *meta = (char *)ctx->buf("lf_meta", nrec + nsub + npre + nblu + 64, &rc, &grew_m);
+    const size_t npre = H.pre.size() * 4, nblu = (std::max<size_t>(1, H.blu.size()) * 4 + 15) / 16 * 16;
+    const size_t ndesc = H.tabs.size() * sizeof(LfTab);
+    bool grew_m = false, grew_w = false, grew_b = false, grew_t = false;
+    char *meta = (char *)ctx->buf("lf_meta", nrec + nsub + npre + nblu + ndesc + 64, &rc, &grew_m);
+    double2 *tab = (double2 *)ctx->buf("lf_tab", (size_t)H.tabsz * sizeof(double2), &rc, &grew_t);
+    bool grew_i = false;
+    int32_t *itab = (int32_t *)ctx->buf("lf_itab", std::max<size_t>(1, H.itab.size()) * 4 + (H.rad.size() + 1) * 4,
+                                        &rc, &grew_i);
     double2 *w1 = (double2 *)ctx->buf("lf_w", (size_t)H.work * 2 * sizeof(double2), &rc, &grew_w);
     double2 *fbt = (double2 *)ctx->buf("lf_fb", (size_t)std::max<int64_t>(1, H.fbsz) * sizeof(double2), &rc, &grew_b);
     if (rc != BPMX_OK) return rc;
@@ -575,22 +787,41 @@ int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, 
     LfSub *d_sub = (LfSub *)(meta + nrec);
     int32_t *d_pre = (int32_t *)(meta + nrec + nsub);
     int32_t *d_blu = (int32_t *)(meta + nrec + nsub + npre);
-    if (!H.uploaded || grew_b || grew_m) {
+    LfTab *d_desc = (LfTab *)(meta + nrec + nsub + npre + nblu);
+    int32_t *d_rad = itab + std::max<size_t>(1, H.itab.size());
+    if (!H.uploaded || grew_b || grew_m || grew_t || grew_i) {
         /* host vectors live in the context until the next plan, past these async copies */
         HIP_TRY(hipMemcpyAsync(d_rec, H.recs.data(), nrec, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_sub, H.subs.data(), nsub, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_pre, H.pre.data(), npre, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_desc, H.tabs.data(), ndesc, hipMemcpyHostToDevice, s));
+        int32_t tmax = 0;
+        for (const LfTab &t : H.tabs) tmax = std::max(tmax, t.count);
+        LAUNCH(ctx, s, "k_lf_tab", k_lf_tab, dim3((unsigned)((tmax + 255) / 256), (unsigned)H.tabs.size()), dim3(256), 0,
+               s, d_desc, tab);
+        if (!H.rad.empty()) {
+            HIP_TRY(hipMemcpyAsync(itab, H.itab.data(), H.itab.size() * 4, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(d_rad, H.rad.data(), H.rad.size() * 4, hipMemcpyHostToDevice, s));
+            size_t bl = 0;
+            for (int32_t i : H.rad) bl = std::max(bl, (size_t)2 * H.subs[i].L * sizeof(double2));
+            (void)hipFuncSetAttribute((const void *)k_lf_rader_b, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bl);
+            LAUNCH(ctx, s, "k_lf_rader_b", k_lf_rader_b, dim3((unsigned)H.rad.size()), dim3(LF_T), bl, s, d_sub, d_rad,
+                   tab, itab, fbt);
+        }
         if (!H.blu.empty()) {
             HIP_TRY(hipMemcpyAsync(d_blu, H.blu.data(), H.blu.size() * 4, hipMemcpyHostToDevice, s));
             size_t bl = 0;
             for (int32_t i : H.blu) bl = std::max(bl, (size_t)2 * H.subs[i].L * sizeof(double2));
             (void)hipFuncSetAttribute((const void *)k_lf_blu_b, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bl);
-            LAUNCH(ctx, s, "k_lf_blu_b", k_lf_blu_b, dim3((unsigned)H.blu.size()), dim3(LF_T), bl, s, d_sub, d_blu, fbt);
+            LAUNCH(ctx, s, "k_lf_blu_b", k_lf_blu_b, dim3((unsigned)H.blu.size()), dim3(LF_T), bl, s, d_sub, d_blu, tab,
+                   fbt);
         }
         H.uploaded = true;
     }
     LfArgs a;
-    a.yd = yd; a.hb = hb; a.w1 = w1; a.w2 = w1 + H.work; a.fbt = fbt; a.rec = d_rec; a.sub = d_sub; a.R = R;
+    a.yd = yd; a.hb = hb; a.w1 = w1; a.w2 = w1 + H.work; a.fbt = fbt; a.tab = tab; a.itab = itab; a.rec = d_rec;
+    a.sub = d_sub;
+    a.R = R;
     const int32_t *P = H.pre.data();
     const unsigned ntile = (unsigned)P[R];
     const unsigned rows_of_A = (unsigned)P[1 * (R + 1) + R];   /* R1 / R1': B rows of A points */
@@ -603,13 +834,13 @@ int longfft_hilbert(bpmx_ctx *ctx, hipStream_t s, const double *yd, double *hb, 
     ar2.pre = d_pre + 2 * (R + 1);
     am.pre = d_pre + 3 * (R + 1);
     LAUNCH(ctx, s, "k_lf_tr", k_lf_tr<1>, dim3(ntile), dim3(256), 0, s, at, (const double2 *)nullptr, a.w1, 0);
-    LAUNCH(ctx, s, "k_lf_rows", k_lf_rows, dim3(rows_of_A), dim3(LF_T), H.lds, s, ar1, a.w1, 1, -1, 1);
+    LAUNCH(ctx, s, "k_lf_rows[A]", k_lf_rows, dim3(rows_of_A), dim3(LF_T), H.lds, s, ar1, a.w1, 1, -1, 1);
     LAUNCH(ctx, s, "k_lf_tr", k_lf_tr<0>, dim3(ntile), dim3(256), 0, s, at, (const double2 *)a.w1, a.w2, 1);
-    LAUNCH(ctx, s, "k_lf_rows", k_lf_rows, dim3(rows_of_B), dim3(LF_T), H.lds, s, ar2, a.w2, 0, -1, 0);
+    LAUNCH(ctx, s, "k_lf_rows[B]", k_lf_rows, dim3(rows_of_B), dim3(LF_T), H.lds, s, ar2, a.w2, 0, -1, 0);
     LAUNCH(ctx, s, "k_lf_mid", k_lf_mid, dim3(nmid), dim3(256), 0, s, am);
-    LAUNCH(ctx, s, "k_lf_rows", k_lf_rows, dim3(rows_of_B), dim3(LF_T), H.lds, s, ar2, a.w2, 0, +1, 1);
+    LAUNCH(ctx, s, "k_lf_rows[B]", k_lf_rows, dim3(rows_of_B), dim3(LF_T), H.lds, s, ar2, a.w2, 0, +1, 1);
     LAUNCH(ctx, s, "k_lf_tr", k_lf_tr<0>, dim3(ntile), dim3(256), 0, s, at, (const double2 *)a.w2, a.w1, 0);
-    LAUNCH(ctx, s, "k_lf_rows", k_lf_rows, dim3(rows_of_A), dim3(LF_T), H.lds, s, ar1, a.w1, 1, +1, 0);
+    LAUNCH(ctx, s, "k_lf_rows[A]", k_lf_rows, dim3(rows_of_A), dim3(LF_T), H.lds, s, ar1, a.w1, 1, +1, 0);
     LAUNCH(ctx, s, "k_lf_tr", k_lf_tr<2>, dim3(ntile), dim3(256), 0, s, at, (const double2 *)a.w1, (double2 *)nullptr, 1);
     return BPMX_OK;
 }

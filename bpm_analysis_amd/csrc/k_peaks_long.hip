@@ -41,6 +41,7 @@ __device__ __forceinline__ int fpl_units(int64_t n) {
 }  // namespace
 
 constexpr int FPL_T = 256;   /* threads of the per-unit kernels: 4 units per workgroup */
+constexpr int FPD_MMAX = 30720;   /* k_fpl_distance: candidates with LDS states and neighbour lists (150 KB) */
 
 __global__ __launch_bounds__(FPL_T) void k_fpl_scan(PeakArgs A, FplArgs L) {
     const int f = blockIdx.y;
@@ -200,6 +201,81 @@ __global__ __launch_bounds__(1024) void k_fpl_distance(PeakArgs A, FplArgs L) {
     }
     const int64_t dist = A.distance;
     if (dist <= 1) return;
+    if (M <= FPD_MMAX) {
+        /* States in LDS and each candidate's higher-priority neighbours listed
+         * once (up to four, as signed index offsets packed in a register; more
+         * or farther: a full scan of mp / mh each round).  Rounds run
+         * wave-locally (a candidate's neighbours are mostly the adjacent lanes)
+         * until the wave makes no progress; one workgroup barrier then lets
+         * decisions cross wave boundaries.  A decision needs a KEPT neighbour
+         * (final) or no UNDECIDED one, so unsynchronised reads only delay it. */
+        __shared__ uint8_t s_st[FPD_MMAX];
+        __shared__ uint32_t s_nb[FPD_MMAX];
+        for (int j = tid; j < M; j += 1024) {
+            s_st[j] = st[j];
+            const int64_t pj = mp[j];
+            const double vj = mh[j];
+            uint32_t w = 0u;
+            int c = 0;
+            bool over = false;
+            auto add = [&](int k) {
+                const int o = k - j;
+                if (c < 4 && o >= -63 && o <= 63) w |= (uint32_t)(o & 127) << (7 * c);
+                else over = true;
+                ++c;
+            };
+            for (int k = j - 1; k >= 0 && pj - mp[k] < dist; --k)
+                if (mh[k] > vj) add(k);
+            for (int k = j + 1; k < M && mp[k] - pj < dist; ++k)
+                if (mh[k] >= vj) add(k);
+            s_nb[j] = w | (uint32_t)(over ? 7 : c) << 28;
+        }
+        __syncthreads();
+        for (int gi = 0; gi <= M; ++gi) {
+            bool pending = false;
+            for (int lr = 0; lr <= M; ++lr) {
+                bool progress = false;
+                pending = false;
+                for (int j = tid; j < M; j += 1024) {
+                    if (ld_state(&s_st[j]) != ST_UNDECIDED) continue;
+                    bool killed = false, blocked = false;
+                    const uint32_t w = s_nb[j];
+                    const int c = (int)(w >> 28);
+                    if (c != 7) {
+                        for (int q = 0; q < c; ++q) {
+                            const int o = (int)((w >> (7 * q)) & 127u);
+                            const int k = j + (o >= 64 ? o - 128 : o);
+                            const uint8_t sk = ld_state(&s_st[k]);
+                            killed |= sk == ST_KEPT;
+                            blocked |= sk == ST_UNDECIDED;
+                        }
+                    } else {
+                        const int64_t pj = mp[j];
+                        const double vj = mh[j];
+                        for (int k = j - 1; k >= 0 && pj - mp[k] < dist && !killed; --k)
+                            if (mh[k] > vj) {
+                                const uint8_t sk = ld_state(&s_st[k]);
+                                killed = sk == ST_KEPT;
+                                blocked |= sk == ST_UNDECIDED;
+                            }
+                        for (int k = j + 1; k < M && mp[k] - pj < dist && !killed; ++k)
+                            if (mh[k] >= vj) {
+                                const uint8_t sk = ld_state(&s_st[k]);
+                                killed = sk == ST_KEPT;
+                                blocked |= sk == ST_UNDECIDED;
+                            }
+                    }
+                    if (killed) { st_state(&s_st[j], ST_REMOVED); progress = true; }
+                    else if (!blocked) { st_state(&s_st[j], ST_KEPT); progress = true; }
+                    else pending = true;
+                }
+                if (!__ballot(progress)) break;                  /* wave-uniform */
+            }
+            if (!__syncthreads_or(pending)) break;
+        }
+        for (int j = tid; j < M; j += 1024) st[j] = s_st[j];
+        return;
+    }
     /* every round decides at least the highest-priority undecided candidate */
     for (int round = 0; round <= M; ++round) {
         if (tid == 0) s_flag = 0;

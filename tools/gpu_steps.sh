@@ -36,6 +36,10 @@ for step in "$@"; do
     fpnat) run dump_env_nat 300 python tools/dump_env.py 1024 native /tmp/env_nat.bin && run fpbench_nat 120 ./tools/fpbench /tmp/env_nat.bin l ;;
     pipesweep_word) BPMX_CUMASK_PER_WORD=1 run pipesweep_word 600 python tools/pipe_sweep.py --steps 10 --shapes 0,0,0 4,192,0 4,224,0 4,192,64 0,0,0 ;;
     pipesweep_grid) run pipesweep_grid 600 python tools/pipe_sweep.py --steps 10 --shapes 0,0,0,0 0,0,0,448 0,0,0,384 0,0,0,320 2,0,0,384 4,0,0,384 2,0,0,320 4,0,0,320 8,0,0,384 0,0,0,0 ;;
+    kprof) run kprof 300 python tools/kprof.py ;;
+    kprof_und) run kprof_und 300 python tools/kprof.py --mult 1.0 && run kprof_und_full 300 python tools/kprof.py --mult 1.0 --options 8 ;;
+    kprof_ref) run kprof_ref 300 python tools/kprof.py --mode reference ;;
+    nbphases) run nb_default 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_nomfma.so run nb_nomfma 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_noepi.so run nb_noepi 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_dma.so run nb_dma 300 python tools/c5_env_prof.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
