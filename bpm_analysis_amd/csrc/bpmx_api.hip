@@ -348,9 +348,10 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             const bool multi = P->channels > 1;
             const dim3 g((F + 63) / 64), b(64);
             const dim3 gp((unsigned)((maxnd + 30 + 63) / 64), (unsigned)((F + 63) / 64));
-            /* b1 = b3 = 0 with integer PCM (always finite): the filter step
-             * skips the two zero products (k_envelope_ref.hip, Df2t::step) */
-            const bool zb = P->ba_b[1] == 0.0 && P->ba_b[3] == 0.0 &&
+            /* b = b0 (1, 0, -2, 0, 1) exactly with integer PCM (always finite):
+             * the filter step's short form (k_envelope_ref.hip, Df2t::step) */
+            const bool zb = P->ba_b[1] == 0.0 && P->ba_b[3] == 0.0 && P->ba_b[4] == P->ba_b[0] &&
+                            P->ba_b[2] == -2.0 * P->ba_b[0] &&
                             (P->dtype == BPMX_DT_U8 || P->dtype == BPMX_DT_I16 || P->dtype == BPMX_DT_I32);
 #define ENV_REF_K(DT, M, Z) LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, M, Z>), g, b, 0, s, a)
 #define ENV_REF(DT)                                                                                  \
@@ -671,7 +672,6 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.dec = tdec; a.exact = d_exact;
             a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
             a.stats = d_stats;
-            a.lu = (double2 *)ctx->buf("trough_lu", (size_t)sumnd * 16, &rc);
             if (rc != BPMX_OK) return rc;
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;

@@ -221,7 +221,6 @@ struct DraftBoundArgs {
     int32_t local_m;         /* more troughs than this: rank segments per window (DB_LOCAL_M) */
     int64_t *stats;          /* optional (BPMX_OPT_STATS): += raw troughs, undecided troughs, chunks sent to the
                                 full draft by draft_point */
-    double2 *lu;             /* [doff + j] scratch: the bracket (L, U) of an undecided trough */
 };
 constexpr int DB_T = 256;
 constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */

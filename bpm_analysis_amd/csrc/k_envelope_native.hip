@@ -656,63 +656,85 @@ template __global__ void k_native_blocks_mfma<3>(NatBlockArgs, const nm_i4 *, co
 template __global__ void k_native_blocks_mfma<5>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *);
 
 /* ---------------------------------------------------------------------- */
-/* int16 mono or stereo beyond k_native_blocks_mfma's K <= 160: the same exact
- * integer GEMM with K = channels x (ds + 1) up to 32 KS.
+
+/* ---------------------------------------------------------------------- */
+/* int16 mono beyond k_native_blocks_mfma's K <= 160, and int16 stereo: the
+ * same exact integer GEMM with K = channels x (ds + 1) <= 640.
  *
  * Stereo enters the K dimension as it lies in memory (L0 R0 L1 R1 ...), each
  * coefficient digit duplicated for the two channels, so one accumulation
  * gives sum_i q_i (L_i + R_i) exactly; the channel mean (bpm_analysis.py:1016,
- * an exact f64 halving) is applied after the one rounding.  The coefficient
- * fragments stay in registers for the whole kernel: one A fragment per M tile
- * and K step serves both halves of the sample split (the high-byte products
- * go to their own accumulators and shift by one digit row when the rows are
- * combined), 8 KS registers.  With K up to 608, |acc| < 2^25, so the digit
- * rows combine in f64 (exact below 2^53) rather than int32.
+ * an exact f64 halving) is applied after the one rounding.  With K up to 640,
+ * |acc| < 2^25, so the digit rows combine in f64 (exact below 2^53).
  *
- * One four-wave workgroup per CU (launch_bounds(256, 1): the fragments need
- * the registers), one LDS-DMA slot of up to 38 KB per wave: tiles of up to 64
- * blocks (mono) or 32 (stereo at ds = 300). */
-constexpr int NB_WAVES = 4;
-inline int nb_ndma() {                                  /* host: DMA wave-instructions per tile (1 KiB each) */
-    const int n = (160 * 1024 - ET_SIZE * 8 - 4 * 64 - 1024) / (NB_WAVES * 1024);
-    return n < 38 ? n : 38;
+ * The coefficient fragments stay in registers (4 M tiles x KS K steps), so a
+ * workgroup is four waves, one per SIMD.  Each wave owns two LDS-DMA slots
+ * (r03): a tile of bt <= 64 blocks arrives as sub-tiles of bs <= 16 blocks,
+ * each into the slot the sub-tile before last used, so while the wave
+ * multiplies one slot the other is in flight, and both fly during the tile's
+ * epilogue.  (The r02 kernel had one 38 KB slot per wave and 32-block stereo
+ * tiles: its DMA, matrix phase and epilogue added up — C5 7.1-7.4 ms against
+ * 4.9 ms for the DMA alone; this one 6.5 ms.)  Eight 19 KB slots per CU hold
+ * 16 stereo blocks each at ds = 300, so the product runs on
+ * v_mfma_i32_16x16x64_i8 (N = 16 blocks, K steps of 64 samples): 4 M tiles
+ * of 16 digit rows, lane l = block l & 15 and K group l >> 4 on B;
+ * accumulator register i of M tile m in lane group g is digit row 4 (m & 1)
+ * + i of coefficient 2 g + (m >> 1), so each lane ends with all digit rows of
+ * two coefficients of its block.  A sub-tile's results move to the lanes of
+ * its blocks (lane = block within the tile) by bpermutes, and the epilogue
+ * runs once per 64 blocks with every lane busy.  Step s + 1's LDS words are
+ * requested before step s's products issue (one wave per SIMD: nothing else
+ * hides the LDS latency). */
+constexpr int NB_WAVES = 4, NB_SLOTS = 2, NB_NDMA = 19;   /* waves, slots per wave, DMA instructions (KiB) per slot */
+__host__ __device__ inline int nb_sub_blocks(int ds, int ch, int ks64, int ndma) {
+    const int hw = ndma * 64 * 8;                    /* halfwords per slot */
+    const int b = (hw - 7 - 64 * ks64 - 2) / (ds * ch) + 1;
+    return b < 16 ? b : 16;                          /* one 16-column N tile per sub-tile */
 }
-__host__ __device__ inline int nb_tile_blocks(int ds, int ch, int ks, int ndma) {
-    const int hw = ndma * 64 * 8;                        /* halfwords per slot */
-    const int b = (hw - 7 - 32 * ks - 2) / (ds * ch) + 1;
-    return b < 64 ? b : 64;
+template <int N>
+__device__ __forceinline__ void nb_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+/* wait until at most k sub-tiles' DMA (k * NDMA instructions) are outstanding */
+template <int NDMA, int K>
+__device__ __forceinline__ void nb_wait_subs(int k) {
+    if constexpr (K == 0) nb_wait_vm<0>();
+    else {
+        if (k >= K) nb_wait_vm<K * NDMA>();
+        else nb_wait_subs<NDMA, K - 1>(k);
+    }
 }
 
-template <int KS>
-__global__ __launch_bounds__(64 * NB_WAVES, 1) void k_native_blocks_mfma_big(NatBlockArgs A, const nm_i4 *__restrict__ afrag,
-                                                                          const nm_i16 *__restrict__ ainit,
-                                                                          const double *__restrict__ cscale, int ndma) {
+template <int KS, int NS, int NDMA, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_native_blocks_mfma_big(NatBlockArgs A, const nm_i4 *__restrict__ afrag,
+                                                                     const nm_i4 *__restrict__ ainit,
+                                                                     const double *__restrict__ cscale, int bs) {
     typedef nat_u4 u4;
     extern __shared__ __align__(16) unsigned char nb_smem[];
     __shared__ double s_et[ET_SIZE];
-    __shared__ nm_i16 s_init[4];
+    __shared__ nm_i4 s_init[4][4];                      /* [M tile][lane group] */
     nat_stage_epilogue_tables(A, s_et);
-    for (int i = threadIdx.x; i < 4; i += blockDim.x) s_init[i] = ainit[(i >> 1) * 64 + (i & 1) * 32];
-    const int lane = lane_id(), hf = lane >> 5, wv = __builtin_amdgcn_readfirstlane(wave_id());
+    for (int i = threadIdx.x; i < 16; i += blockDim.x) s_init[i >> 2][i & 3] = ainit[i];
+    const int lane = lane_id(), g4 = lane >> 4, wv = __builtin_amdgcn_readfirstlane(wave_id());
     const int16_t *pcm = (const int16_t *)A.pcm;
     const int64_t total = A.total;                        /* int16 elements */
     const int ds = A.ds, bt = A.bt, ch = A.channels, bstride = ds * ch;
-    const int slot_ch = ndma * 64;
-    u4 *slot = (u4 *)nb_smem + wv * slot_ch;
-    const int nch = (7 + bt * bstride + ch + 7) >> 3;    /* chunks a tile may touch */
-    nm_i4 af[2][KS];
+    constexpr int SLOT_CH = NDMA * 64;
+    u4 *const slots = (u4 *)nb_smem + NS * wv * SLOT_CH;
+    const int nch = (7 + bs * bstride + ch + 7) >> 3;    /* chunks a sub-tile may touch (<= SLOT_CH) */
+    nm_i4 af[4][KS];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int s = 0; s < KS; ++s) af[t][s] = afrag[(t * KS + s) * 64 + lane];
-    double sc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sc[q] = cscale[2 * q + hf] * (ch == 2 ? 0.5 : 1.0);   /* exact */
+        for (int s = 0; s < KS; ++s) af[m][s] = afrag[(m * KS + s) * 64 + lane];
+    const double sc0 = cscale[2 * g4] * (ch == 2 ? 0.5 : 1.0), sc1 = cscale[2 * g4 + 1] * (ch == 2 ? 0.5 : 1.0);   /* exact */
     __syncthreads();
     const int64_t clast = (total & ~(int64_t)7) - 8;
-    auto dma = [&](int64_t e0) {
+    /* exactly NDMA instructions per sub-tile, every lane on (the vmcnt
+     * waits below count them); chunks past the sub-tile re-read the batch's
+     * last whole chunk */
+    auto dma = [&](int64_t e0, u4 *slot) {
         const int64_t a0 = e0 & ~(int64_t)7;
-        for (int r = 0; r < ndma; ++r) {
+#pragma unroll
+        for (int r = 0; r < NDMA; ++r) {
             const int q = r * 64 + lane;
             int64_t c = a0 + (int64_t)q * 8;
             c = (q < nch && c + 8 <= total) ? c : clast;
@@ -721,99 +743,134 @@ __global__ __launch_bounds__(64 * NB_WAVES, 1) void k_native_blocks_mfma_big(Nat
                          :: "v"(pcm + c), "s"(m0) : "memory");
         }
     };
-    const int64_t stride = (int64_t)gridDim.x * NB_WAVES;
-    int64_t t = (int64_t)blockIdx.x * NB_WAVES + wv;
-    NatTile tl{};
-    if (t < A.n_tiles) {
-        tl = nat_tile_ld(A.tiles, t);
-        dma(tl.s0 * ch);
-    }
-    for (; t < A.n_tiles; t += stride) {
-        const int64_t tr = t + stride;
-        NatTile tn{};
-        if (tr < A.n_tiles) tn = nat_tile_ld(A.tiles, tr);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int64_t e0 = tl.s0 * ch;
-        const int coff = (int)(e0 & 7);
-        {
-            const int64_t a0 = e0 - coff, tail0 = total & ~(int64_t)7;
-            if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))   /* last tile of the batch */
-                ((int16_t *)slot)[tail0 - a0 + lane] = pcm[tail0 + lane];
-            __builtin_amdgcn_wave_barrier();
+    auto nsub_of = [&](const NatTile &h) {
+        const int Lt = h.nb - h.j0 < bt ? h.nb - h.j0 : bt;
+        return (Lt + bs - 1) / bs;
+    };
+    const int64_t stride = (int64_t)gridDim.x * NW, t0 = (int64_t)blockIdx.x * NW + wv;
+    /* producer: the next sub-tile to fetch (tile pt, sub-tile pu) */
+    int64_t pt = t0;
+    int pu = 0;
+    NatTile ptl{};
+    if (pt < A.n_tiles) ptl = nat_tile_ld(A.tiles, pt);
+    int64_t issued = 0;
+    auto produce = [&](u4 *slot) {
+        dma((ptl.s0 + (int64_t)pu * bs * ds) * ch, slot);
+        ++issued;
+        if (++pu >= nsub_of(ptl)) {
+            pu = 0;
+            pt += stride;
+            if (pt < A.n_tiles) ptl = nat_tile_ld(A.tiles, pt);
         }
+    };
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+        if (pt < A.n_tiles) produce(slots + k * SLOT_CH);
+    int64_t g = 0;                                        /* sub-tiles consumed */
+    for (int64_t t = t0; t < A.n_tiles; t += stride) {
+        const NatTile tl = nat_tile_ld(A.tiles, t);
         const int Lt = tl.nb - tl.j0 < bt ? tl.nb - tl.j0 : bt;
-        const uint32_t *tw = (const uint32_t *)slot;
-        double res[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        const int ns = (Lt + bs - 1) / bs;
+        double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double x0 = 0.0;
+        for (int u = 0; u < ns; ++u, ++g) {
+            u4 *slot = slots + (int)(g % NS) * SLOT_CH;
+            /* DMAs retire in issue order: with k later sub-tiles in flight,
+             * <= k NDMA outstanding means this one landed (the epilogue's few
+             * stores, issued later, only make it over-wait) */
+            nb_wait_subs<NDMA, NS - 1>((int)(issued - g - 1));
+            const int64_t e0 = (tl.s0 + (int64_t)u * bs * ds) * ch;
+            const int coff = (int)(e0 & 7);
+            {
+                const int64_t a0 = e0 - coff, tail0 = total & ~(int64_t)7;
+                if ((total & 7) && a0 + (int64_t)nch * 8 > tail0 && lane < (int)(total & 7))   /* batch's last chunk */
+                    ((int16_t *)slot)[tail0 - a0 + lane] = pcm[tail0 + lane];
+                __builtin_amdgcn_wave_barrier();
+            }
+            const int Ls = Lt - u * bs < bs ? Lt - u * bs : bs;
+            const uint32_t *tw = (const uint32_t *)slot;
+            double val0, val1;                            /* coefficients 2 g4, 2 g4 + 1 of block lane & 15 */
+            {
+                const int b = lane & 15;
+                const int hw0 = coff + (b < Ls ? b : 0) * bstride + 16 * g4;
+                const uint32_t sh = (hw0 & 1) ? 16u : 0u;
+                nm_i4 l[4], h[4];
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            if (n == 1 && Lt <= 32) break;                   /* wave-uniform */
-            const int b = 32 * n + (lane & 31);
-            const int hw0 = coff + (b < Lt ? b : 0) * bstride + 16 * hf;
-            const uint32_t sh = (hw0 & 1) ? 16u : 0u;
-            nm_i16 l0 = s_init[hf], l1 = s_init[2 + hf];
-            nm_i16 h0 = {}, h1 = {};
+                for (int m = 0; m < 4; ++m) { l[m] = s_init[m][g4]; h[m] = nm_i4{0, 0, 0, 0}; }
 #ifndef BPMX_NB_SKIP_MFMA            /* diagnostic builds (tools/build_variant.sh): phase timing */
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const uint32_t *p = tw + ((hw0 + 32 * s) >> 1);
+                const uint32_t *p = tw + (hw0 >> 1);
                 uint32_t w[9];
 #pragma unroll
                 for (int i = 0; i < 9; ++i) w[i] = p[i];
-                nm_i4 bh, bl;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t e0w = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sh);
-                    const uint32_t e1w = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sh);
-                    bh[i] = (int32_t)__builtin_amdgcn_perm(e1w, e0w, 0x07050301u);
-                    bl[i] = (int32_t)(__builtin_amdgcn_perm(e1w, e0w, 0x06040200u) ^ 0x80808080u);
+                for (int s = 0; s < KS; ++s) {
+                    nm_i4 bh, bl;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t e0w = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sh);
+                        const uint32_t e1w = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sh);
+                        bh[i] = (int32_t)__builtin_amdgcn_perm(e1w, e0w, 0x07050301u);
+                        bl[i] = (int32_t)(__builtin_amdgcn_perm(e1w, e0w, 0x06040200u) ^ 0x80808080u);
+                    }
+                    if (s + 1 < KS) {
+#pragma unroll
+                        for (int i = 0; i < 9; ++i) w[i] = p[32 * (s + 1) + i];
+                    }
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        l[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m][s], bl, l[m], 0, 0, 0);
+                        h[m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m][s], bh, h[m], 0, 0, 0);
+                    }
                 }
-                l0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s], bl, l0, 0, 0, 0);
-                l1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s], bl, l1, 0, 0, 0);
-                h0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s], bh, h0, 0, 0, 0);
-                h1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s], bh, h1, 0, 0, 0);
-            }
 #else
-            l0[0] = (int)tw[hw0 >> 1];
+                l[0][0] = (int)tw[hw0 >> 1];
 #endif
-            /* digit rows R_r = l_r + h_(r-1) (l: rows 0-3 in l0, 4-7 in l1) */
+                /* digit rows R_r = l_r + h_(r-1): coefficient 2 g4 + k has rows 0-3 in M tile 2k, 4-7 in 2k + 1 */
+                double v2[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const nm_i4 la = l[2 * k], lb = l[2 * k + 1], ha = h[2 * k], hb = h[2 * k + 1];
+                    const double r0 = (double)la[0], r1 = (double)(la[1] + ha[0]);
+                    const double r2 = (double)(la[2] + ha[1]), r3 = (double)(la[3] + ha[2]);
+                    const double r4 = (double)(lb[0] + ha[3]), r5 = (double)(lb[1] + hb[0]);
+                    const double r6 = (double)(lb[2] + hb[1]), r7 = (double)(lb[3] + hb[2]);
+                    const double L = __builtin_fma(r3, 16777216.0, __builtin_fma(r2, 65536.0, __builtin_fma(r1, 256.0, r0)));
+                    const double H = __builtin_fma(r7, 16777216.0, __builtin_fma(r6, 65536.0, __builtin_fma(r5, 256.0, r4)));
+                    v2[k] = __builtin_fma(H, 4294967296.0, L);
+                }
+                val0 = v2[0] * sc0;
+                val1 = v2[1] * sc1;
+            }
+            /* this sub-tile's blocks are tile lanes [u bs, u bs + Ls) */
+            const int c = lane - u * bs;
+            const bool mine = c >= 0 && c < Ls;
+            if (mine) {
+                const int16_t *fr = (const int16_t *)slot + coff + c * bstride;
+                x0 = ch == 2 ? 0.5 * (double)((int)fr[0] + (int)fr[1]) : (double)fr[0];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the slot is read: refill it */
+            if (pt < A.n_tiles) produce(slot);
+            const int src = mine ? c : 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double r0 = (double)l0[4 * q], r1 = (double)(l0[4 * q + 1] + h0[4 * q]);
-                const double r2 = (double)(l0[4 * q + 2] + h0[4 * q + 1]), r3 = (double)(l0[4 * q + 3] + h0[4 * q + 2]);
-                const double r4 = (double)(l1[4 * q] + h0[4 * q + 3]), r5 = (double)(l1[4 * q + 1] + h1[4 * q]);
-                const double r6 = (double)(l1[4 * q + 2] + h1[4 * q + 1]), r7 = (double)(l1[4 * q + 3] + h1[4 * q + 2]);
-                const double L = __builtin_fma(r3, 16777216.0, __builtin_fma(r2, 65536.0, __builtin_fma(r1, 256.0, r0)));
-                const double H = __builtin_fma(r7, 16777216.0, __builtin_fma(r6, 65536.0, __builtin_fma(r5, 256.0, r4)));
-                res[n][q] = __builtin_fma(H, 4294967296.0, L) * sc[q];
+                const double e = __shfl(val0, src + 16 * q), o = __shfl(val1, src + 16 * q);
+                if (mine) { cf[2 * q] = e; cf[2 * q + 1] = o; }
             }
         }
         const int j = tl.j0 + lane;
         const bool valid = lane < bt && j < tl.nb;
-        double x0 = 0.0;
-        if (valid) {
-            const int16_t *fr = (const int16_t *)slot + coff + lane * bstride;
-            x0 = ch == 2 ? 0.5 * (double)((int)fr[0] + (int)fr[1]) : (double)fr[0];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the slot is read: refill it */
-        if (tr < A.n_tiles) dma(tn.s0 * ch);
-        double cf[8];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const double other = __shfl_xor(hf ? res[0][q] : res[1][q], 32);
-            cf[2 * q] = hf ? other : res[0][q];
-            cf[2 * q + 1] = hf ? res[1][q] : other;
-        }
 #ifndef BPMX_NB_SKIP_EPI
         nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{cf[0], cf[1], cf[2], cf[3]}, V4{cf[4], cf[5], cf[6], cf[7]},
                           x0);
 #else
         if (valid && cf[0] == 12345.0) A.gam[0] = x0;
 #endif
-        tl = tn;
     }
 }
-template __global__ void k_native_blocks_mfma_big<10>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *, int);
-template __global__ void k_native_blocks_mfma_big<19>(NatBlockArgs, const nm_i4 *, const nm_i16 *, const double *, int);
+template __global__ void k_native_blocks_mfma_big<5, NB_SLOTS, NB_NDMA, NB_WAVES>(NatBlockArgs, const nm_i4 *, const nm_i4 *,
+                                                                                const double *, int);
+template __global__ void k_native_blocks_mfma_big<10, NB_SLOTS, NB_NDMA, NB_WAVES>(NatBlockArgs, const nm_i4 *, const nm_i4 *,
+                                                                                 const double *, int);
 
 /* ---------------------------------------------------------------------- */
 /* int16 interleaved PCM (stereo; also mono beyond the matrix-core path's
@@ -1659,11 +1716,12 @@ std::vector<int32_t> build_mfma(const std::vector<LD> &cl, int R, int KS) {
     return w;
 }
 
-/* tables for k_native_blocks_mfma_big: as build_mfma, K = CH x R with each
- * coefficient repeated for the CH interleaved channels, and one A fragment
- * per (M tile, K step) carrying digit rows 4t + i (the high-byte products
- * are shifted by a row when the accumulators combine):
- *   [0, 16) scale | [16, 16 + 2*64*16) initial accumulators | [t][K step][lane][4 words] */
+/* tables for k_native_blocks_mfma_big (v_mfma_i32_16x16x64_i8), the digits of build_mfma
+ * with K = CH x R, each coefficient repeated for the CH interleaved channels:
+ *   [0, 16) scale | [16, 80) initial accumulators [M tile m][lane group g][4]
+ *   | A fragments [m][K step][lane][4 words]
+ * M tile m, row rho = 4 g + i: coefficient 2 g + (m >> 1), digit row 4 (m & 1) + i;
+ * lane l of a fragment: row l & 15, K = 64 step + 16 (l >> 4) + byte. */
 std::vector<int32_t> build_mfma_big(const std::vector<LD> &cl, int R, int KS, int CH) {
     std::vector<int64_t> q((size_t)R * 8);
     std::vector<double> scale(8);
@@ -1689,27 +1747,27 @@ std::vector<int32_t> build_mfma_big(const std::vector<LD> &cl, int R, int KS, in
     auto dig = [&](int k, int c, int r) -> int {
         return (k < K && r >= 0 && r < 8) ? d[((size_t)(k / CH) * 8 + c) * 8 + r] : 0;
     };
-    std::vector<int32_t> w(16 + 2 * 64 * 16 + (size_t)2 * KS * 64 * 4, 0);
+    std::vector<int32_t> w(16 + 64 + (size_t)4 * KS * 64 * 4, 0);
     std::memcpy(w.data(), scale.data(), 64);
     int32_t *init = w.data() + 16;
-    for (int t = 0; t < 2; ++t)
-        for (int l = 0; l < 64; ++l)
-            for (int reg = 0; reg < 16; ++reg) {
-                const int c = 2 * (reg >> 2) + (l >> 5), r = 4 * t + (reg & 3);
+    for (int m = 0; m < 4; ++m)
+        for (int g = 0; g < 4; ++g)
+            for (int i = 0; i < 4; ++i) {
+                const int c = 2 * g + (m >> 1), r = 4 * (m & 1) + i;
                 int64_t sum = 0;
                 for (int k = 0; k < K; ++k) sum += dig(k, c, r);
-                init[(t * 64 + l) * 16 + reg] = (int32_t)(128 * sum);
+                init[(m * 4 + g) * 4 + i] = (int32_t)(128 * sum);
             }
-    int32_t *af = init + 2 * 64 * 16;
-    for (int t = 0; t < 2; ++t)
+    int32_t *af = init + 64;
+    for (int m = 0; m < 4; ++m)
         for (int st = 0; st < KS; ++st)
             for (int l = 0; l < 64; ++l) {
-                const int rho = l & 31;
-                const int c = 2 * (rho >> 3) + ((rho >> 2) & 1), r = 4 * t + (rho & 3);
+                const int rho = l & 15;
+                const int c = 2 * (rho >> 2) + (m >> 1), r = 4 * (m & 1) + (rho & 3);
                 for (int j = 0; j < 16; ++j) {
-                    const int k = 32 * st + 16 * (l >> 5) + j;
+                    const int k = 64 * st + 16 * (l >> 4) + j;
                     const uint32_t byte = (uint8_t)(int8_t)dig(k, c, r);
-                    af[((t * KS + st) * 64 + l) * 4 + j / 4] |= (int32_t)(byte << (8 * (j & 3)));
+                    af[((m * KS + st) * 64 + l) * 4 + j / 4] |= (int32_t)(byte << (8 * (j & 3)));
                 }
             }
     return w;
@@ -1771,19 +1829,18 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                           !(P->options & (BPMX_OPT_NATIVE_F64 | BPMX_OPT_NATIVE_DMA));
     const bool use_mfma = mfma_ks && i16_fast && P->channels == 1;
     /* int16 mono beyond K = 160 and int16 stereo: the big-K matrix-core kernel
-     * (K = channels x (ds + 1) <= 608) */
+     * (K = channels x (ds + 1) <= 640, K steps of 64) */
     const int kbig = P->channels * (ds + 1);
-    const int big_ks = kbig <= 320 ? 10 : (kbig <= 608 ? 19 : 0);
-    const int nbdma = nb_ndma();
-    const bool use_big = !use_mfma && i16_fast && big_ks && (P->channels == 1 || P->channels == 2) &&
-                         nb_tile_blocks(ds, P->channels, big_ks, nbdma) >= 1;
+    const int big_ks = kbig <= 320 ? 5 : (kbig <= 640 ? 10 : 0);
+    const int big_bs = big_ks ? nb_sub_blocks(ds, P->channels, big_ks, NB_NDMA) : 0;
+    const bool use_big = !use_mfma && i16_fast && big_ks && (P->channels == 1 || P->channels == 2) && big_bs >= 1;
     /* the rest of int16 stereo (and, on request, mono) through the LDS-DMA f64 kernel */
     const bool use_dma = !use_mfma && !use_big && P->dtype == BPMX_DT_I16 && aligned16 && foff[F] * P->channels >= 16 &&
                          (P->channels == 2 || (P->channels == 1 && (P->options & BPMX_OPT_NATIVE_DMA))) &&
                          !(P->options & BPMX_OPT_NATIVE_F64) && nd_tile_blocks(ds, P->channels) >= 1;
     /* tiles of bt blocks: the LDS tile (slot) must hold the tile's samples */
     const int bt = use_mfma ? nm_tile_blocks(ds, mfma_ks)
-                 : use_big  ? nb_tile_blocks(ds, P->channels, big_ks, nbdma)
+                 : use_big  ? big_bs * (64 / big_bs)
                  : (use_dma ? nd_tile_blocks(ds, P->channels) : std::min(64, (NB_RCH * 512 - 16) / ds));
     std::vector<int64_t> key(17);
     for (int i = 0; i < 12; ++i) std::memcpy(&key[i], &P->sos[i], 8);
@@ -1887,20 +1944,19 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         } else if (use_big) {
             a.total = foff[F] * P->channels;                 /* int16 elements */
             const double *mt = d_tab + mfma_off;
-            const nm_i16 *init = (const nm_i16 *)(mt + 8);
-            const nm_i4 *af = (const nm_i4 *)(mt + 8 + 2 * 64 * 16 / 2);
+            const nm_i4 *init = (const nm_i4 *)(mt + 8), *af = (const nm_i4 *)(mt + 8 + 32);
             const unsigned g1 = (unsigned)std::min<int64_t>((nt + NB_WAVES - 1) / NB_WAVES, 256);
-            const size_t lds = (size_t)nbdma * NB_WAVES * 1024;
-            if (big_ks == 10) {
-                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<10>,
+            const size_t lds = (size_t)NB_SLOTS * NB_NDMA * NB_WAVES * 1024;
+            if (big_ks == 5) {
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<5, NB_SLOTS, NB_NDMA, NB_WAVES>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma_big<10>, dim3(g1), dim3(64 * NB_WAVES), lds, s,
-                       a, af, init, mt, nbdma);
+                LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_mfma_big<5, NB_SLOTS, NB_NDMA, NB_WAVES>), dim3(g1),
+                       dim3(64 * NB_WAVES), lds, s, a, af, init, mt, big_bs);
             } else {
-                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<19>,
+                (void)hipFuncSetAttribute((const void *)k_native_blocks_mfma_big<10, NB_SLOTS, NB_NDMA, NB_WAVES>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                LAUNCH(ctx, s, "k_native_blocks", k_native_blocks_mfma_big<19>, dim3(g1), dim3(64 * NB_WAVES), lds, s,
-                       a, af, init, mt, nbdma);
+                LAUNCH(ctx, s, "k_native_blocks", (k_native_blocks_mfma_big<10, NB_SLOTS, NB_NDMA, NB_WAVES>), dim3(g1),
+                       dim3(64 * NB_WAVES), lds, s, a, af, init, mt, big_bs);
             }
         } else if (use_dma) {
             a.total = foff[F] * P->channels;                 /* int16 elements */

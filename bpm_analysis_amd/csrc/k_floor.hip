@@ -709,14 +709,9 @@ __device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int64_t lo, in
  * trough values): the recording then gets the full draft. */
 constexpr int DP_SPL = 4;
 
-/* wave total of an int (DPP scan, lane 63 read as a scalar) */
-__device__ __forceinline__ int wave_total_dpp(int x) {
-    return __builtin_amdgcn_readlane(wave_iscan_dpp<false>(x), 63);
-}
-
 __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s_tv, int base, int m, int64_t n,
                                             int64_t lo, int64_t hi, int jl, int jh, double q, uint32_t seed,
-                                            double bl, double bu, double *res) {
+                                            double *res) {
     const int lane = lane_id();
     if (jh - jl + 1 > 64 * DP_SPL) return false;
     int32_t sa[DP_SPL], sn[DP_SPL], st[DP_SPL], slo[DP_SPL], shi[DP_SPL], sub[DP_SPL];
@@ -751,28 +746,6 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
         if (scst[r] || x == st[r]) return sy[r];
         return ssl[r] * ((double)x - (double)st[r]) + sy[r];
     };
-    /* the number of segment r's values below v (STRICT: <= v): the linear
-     * formula's inverse gives the index to within rounding, then exact
-     * comparisons step it into place (a bisection if that is far off) */
-    auto count_below = [&](int r, double v, bool le) -> int {
-        const int len = sn[r];
-        auto below = [&](int i) -> bool { const double x = sorted(r, i); return le ? x <= v : x < v; };
-        if (len == 0) return 0;
-        if (scst[r] || ssl[r] == 0.0) return below(0) ? len : 0;
-        const double d0 = (double)(sa[r] - st[r]), u = (v - sy[r]) / ssl[r];
-        double e = sinc[r] ? u - d0 : d0 + (double)(len - 1) - u;
-        e = e < 0.0 ? 0.0 : (e > (double)len ? (double)len : e);
-        int g = (int)ceil(e);
-        for (int it = 0; it < 2; ++it) {
-            if (g < len && below(g)) ++g;
-            else if (g > 0 && !below(g - 1)) --g;
-            else return g;
-        }
-        if ((g >= len || !below(g)) && (g == 0 || below(g - 1))) return g;
-        int l = 0, h = len;                                   /* far off: bisect */
-        while (l < h) { const int mid = (l + h) >> 1; if (below(mid)) l = mid + 1; else h = mid; }
-        return l;
-    };
     const int64_t nobs = hi - lo;
     double idxf = 0.0;
     int64_t k = 0;
@@ -781,19 +754,7 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
         k = (int64_t)idxf;
     }
     const bool interp = !(nobs == 1 || (double)k == idxf);
-    /* start from k_draft_bounds' bracket bl <= s_k <= s_(k+1) <= bu, widened by
-     * 2^-40 relative (a segment's rounded values may step an ulp past its end
-     * values): only the values inside it stay active */
-    const double lw = bl > 0.0 ? bl * (1.0 - 0x1p-40) : -__builtin_inf();
-    const double uw = bu > 0.0 ? bu * (1.0 + 0x1p-40) : __builtin_inf();
-    int nbelow = 0;
-#pragma unroll
-    for (int r = 0; r < DP_SPL; ++r) {
-        slo[r] = count_below(r, lw, false);
-        shi[r] = max(slo[r], count_below(r, uw, true));
-        nbelow += slo[r];
-    }
-    int64_t below = wave_total_dpp(nbelow), leq = -1;
+    int64_t below = 0, leq = -1;
     double va = 0.0;
     uint32_t rng = seed;
     for (int it = 0; it < 256; ++it) {
@@ -801,7 +762,7 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
 #pragma unroll
         for (int r = 0; r < DP_SPL; ++r) cnt += shi[r] - slo[r];
         const int incl = wave_iscan_dpp<false>(cnt);
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        const int tot = __shfl(incl, 63);
         if (tot <= 0) return false;
         rng = rng * 1664525u + 1013904223u;
         const int p = (int)(((uint64_t)rng * (uint64_t)tot) >> 32);
@@ -818,22 +779,21 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
                 off -= c;
             }
         }
-        const uint64_t pb = (uint64_t)__double_as_longlong(pvl);
-        const double pv = __longlong_as_double((long long)(
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pb >> 32), owner) << 32) |
-            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pb, owner)));
+        const double pv = __shfl(pvl, owner);
         int slb[DP_SPL];
         int cl = 0, ce = 0;
 #pragma unroll
         for (int r = 0; r < DP_SPL; ++r) {
-            /* the active range is a contiguous run of ranks, so the counts clamp */
-            const int gl = count_below(r, pv, false), ge = count_below(r, pv, true);
-            slb[r] = min(max(gl, slo[r]), shi[r]);
-            sub[r] = min(max(ge, slb[r]), shi[r]);
+            int l = slo[r], h = shi[r];
+            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) < pv) l = mid + 1; else h = mid; }
+            slb[r] = l;
+            h = shi[r];
+            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) <= pv) l = mid + 1; else h = mid; }
+            sub[r] = l;
             cl += slb[r] - slo[r];
             ce += sub[r] - slo[r];
         }
-        const int64_t nless = below + wave_total_dpp(cl), nleq = below + wave_total_dpp(ce);
+        const int64_t nless = below + wave_sum_i(cl), nleq = below + wave_sum_i(ce);
         if (k < nless) {
 #pragma unroll
             for (int r = 0; r < DP_SPL; ++r) shi[r] = slb[r];
@@ -1060,7 +1020,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         uint8_t dcs;
         if (et <= A.mult * L) dcs = 1;
         else if (et > A.mult * U * (1.0 + 0x1p-50)) dcs = 0;
-        else { dcs = 2; any_undecided = true; A.lu[d0 + j] = make_double2(L, U); }
+        else { dcs = 2; any_undecided = true; }
         A.dec[d0 + j] = dcs;
     }
     if (any_undecided) s_undecided = 1;
@@ -1084,9 +1044,8 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         win_bounds(qp, n, W, s, e);
         const int64_t lo = s > t0 ? s : t0, hi = e;
         double r = 0.0;
-        const double2 bracket = A.lu[d0 + j];
         if (!draft_point(s_tp, s_tv, base, m, n, lo, hi, seg_of(lo), seg_of(hi - 1), A.q,
-                         0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu, bracket.x, bracket.y, &r)) {
+                         0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu, &r)) {
             fail = true;
             continue;
         }
