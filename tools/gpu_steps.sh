@@ -40,6 +40,8 @@ for step in "$@"; do
     kprof_und) run kprof_und 300 python tools/kprof.py --mult 1.0 && run kprof_und_full 300 python tools/kprof.py --mult 1.0 --options 8 ;;
     kprof_ref) run kprof_ref 300 python tools/kprof.py --mode reference ;;
     nbphases) run nb_default 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_nomfma.so run nb_nomfma 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_noepi.so run nb_noepi 300 python tools/c5_env_prof.py && BPMX_LIB=build_var/libbpmx_nb_dma.so run nb_dma 300 python tools/c5_env_prof.py ;;
+    c5ctx) run bench_c5_64_k1 600 python bench.py --workload c5 --c5-files 64 --steps 10 --warmup 2 --c5-contexts 1 --c5-parity-files 0 && run bench_c5_64_k3 600 python bench.py --workload c5 --c5-files 64 --steps 10 --warmup 2 --c5-contexts 3 --c5-parity-files 0 && run bench_c5_64_k2 600 python bench.py --workload c5 --c5-files 64 --steps 10 --warmup 2 --c5-contexts 2 --c5-parity-files 0 ;;
+    c5conc) run c5_concurrency 600 python tools/c5_concurrency.py 3 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
