@@ -414,9 +414,13 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         if (rc != BPMX_OK) return rc;
         fl.b32h = b32; fl.b32l = b32 + n32; fl.b32r = b32 + 2 * n32;
         fl.b1kh = b1k; fl.b1kl = b1k + n1k; fl.b1kr = b1k + 2 * n1k;
+        fl.dfail = (int32_t *)ctx->buf("fpl_dfail", (size_t)F * 4, &rc);
+        if (rc != BPMX_OK) return rc;
+        fl.dchunk = 1;
     }
     const dim3 g_unit((unsigned)((((maxnd - 2 + FPL_U - 1) / FPL_U) + 3) / 4), (unsigned)F);
     const dim3 g_prom((unsigned)((maxnd / 2 + 1 + 255) / 256), (unsigned)F);
+    const dim3 g_dch((unsigned)((maxnd / 2 + 1 + FPC_S - 1) / FPC_S), (unsigned)F);
 #define FIND_PEAKS(A, TAG)                                                                                  \
     do {                                                                                                   \
         (A).vcand = vcand; (A).fallback = fp_fb; (A).only = nullptr;                                      \
@@ -429,6 +433,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             LAUNCH(ctx, s, "k_fpl_scan[" TAG "]", k_fpl_scan, g_unit, dim3(256), 0, s, (A), fl);          \
             LAUNCH(ctx, s, "k_fpl_place[" TAG "]", k_fpl_place, dim3(F), dim3(256), 0, s, (A), fl);       \
             LAUNCH(ctx, s, "k_fpl_fill[" TAG "]", k_fpl_fill, g_unit, dim3(256), 0, s, (A), fl);          \
+            LAUNCH(ctx, s, "k_fpl_dist_ch[" TAG "]", k_fpl_dist_ch, g_dch, dim3(FPC_T), 0, s, (A), fl);   \
             LAUNCH(ctx, s, "k_fpl_distance[" TAG "]", k_fpl_distance, dim3(F), dim3(1024), 0, s, (A), fl);\
             LAUNCH(ctx, s, "k_fpl_prom[" TAG "]", k_fpl_prom, g_prom, dim3(256), 0, s, (A), fl);          \
             LAUNCH(ctx, s, "k_fpl_compact[" TAG "]", k_fpl_compact, dim3(F), dim3(1024), 0, s, (A), fl);  \

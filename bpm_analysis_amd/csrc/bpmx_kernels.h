@@ -134,13 +134,21 @@ struct FplArgs {
     double *vv;            /* [sumNd + F] gap valleys: vv[g] = valley between maxima g-1 and g */
     double *b32h, *b32l, *b32r;    /* per 32 maxima: max height, min vv[k+1], min vv[k] */
     double *b1kh, *b1kl, *b1kr;    /* per 1024 maxima: the same */
+    int32_t *dfail;        /* [F] k_fpl_dist_ch could not cut the recording's maxima into chunks (k_fpl_distance decides it) */
+    int32_t dchunk;        /* k_fpl_dist_ch ran (1): k_fpl_distance only decides recordings with dfail set */
 };
+/* k_fpl_dist_ch: the distance rounds of a long recording in chunks of about
+ * FPC_S maxima, cut where consecutive maxima lie >= distance apart (no
+ * candidate has a neighbour across the cut), a chunk reaching at most FPC_H
+ * maxima past its nominal end */
+constexpr int FPC_T = 256, FPC_S = 1024, FPC_H = 1024, FPC_R = (FPC_S + FPC_H) / FPC_T;
 __host__ __device__ inline int64_t fpl_b32_off(int64_t d0, int f) { return (d0 >> 5) + 4 * (int64_t)f; }
 __host__ __device__ inline int64_t fpl_b1k_off(int64_t d0, int f) { return (d0 >> 10) + 4 * (int64_t)f; }
 __global__ void k_fpl_scan(PeakArgs A, FplArgs L);
 __global__ void k_fpl_place(PeakArgs A, FplArgs L);
 __global__ void k_fpl_fill(PeakArgs A, FplArgs L);
 __global__ void k_fpl_distance(PeakArgs A, FplArgs L);
+__global__ void k_fpl_dist_ch(PeakArgs A, FplArgs L);
 __global__ void k_fpl_prom(PeakArgs A, FplArgs L);
 __global__ void k_fpl_compact(PeakArgs A, FplArgs L);
 

@@ -800,7 +800,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
      * candidate is removed once a higher-priority candidate within `dist` is
      * kept, kept once none is undecided).  Positions and heights do not
      * change, so each candidate's higher-priority neighbours (left: strictly
-     * higher, right: at least as high) are listed once, up to four in
+     * higher, right: at least as high) are listed once, up to eight (8-bit offsets) in
      * registers; a round then only reads their states. */
 #ifdef BPMX_FP_NODIST
     if (false) {
@@ -808,8 +808,9 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     if (dist > 1) {
 #endif
         constexpr int FP_R = FL_MC / FP_T;
-        uint32_t nb[FP_R][2];                                /* four 16-bit neighbour indices */
-        int nbc[FP_R];                                       /* count; -1: more than four (full scan) */
+        constexpr int FP_NB = 8;                             /* neighbours listed per candidate */
+        uint32_t nb[FP_R][2];                                /* eight signed 8-bit offsets k - j */
+        int nbc[FP_R];                                       /* count; -1: more than eight or too far (full scan) */
 #pragma unroll
         for (int r = 0; r < FP_R; ++r) {
             const int j = tid + r * FP_T;
@@ -820,14 +821,16 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
             const double vj = s_mh[j];
             int c = 0;
             auto add = [&](int k) {
-                if (c < 4) nb[r][c >> 1] |= (uint32_t)k << (16 * (c & 1));
+                const int o = k - j;
+                if (o < -128 || o > 127) c = FP_NB;          /* forces the full scan */
+                if (c < FP_NB) nb[r][c >> 2] |= ((uint32_t)o & 0xFFu) << (8 * (c & 3));
                 ++c;
             };
             for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k)
                 if (s_mh[k] > vj && s_st[k] == ST_UNDECIDED) add(k);
             for (int k = j + 1; k < M && s_mp[k] - pj < dist; ++k)
                 if (s_mh[k] >= vj && s_st[k] == ST_UNDECIDED) add(k);
-            nbc[r] = c <= 4 ? c : -1;
+            nbc[r] = c <= FP_NB ? c : -1;
         }
         STAMP(6);
         /* Rounds run wave-locally (a candidate's neighbours are mostly in its
@@ -835,24 +838,39 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
          * workgroup barrier then lets decisions cross wave boundaries.  A
          * decision needs a KEPT neighbour (final) or no UNDECIDED one (a stale
          * read only delays it), so unsynchronised reads are safe. */
+        /* this thread's undecided entries: only it writes their states */
+        uint32_t und = 0u;
+#pragma unroll
+        for (int r = 0; r < FP_R; ++r) {
+            const int j = tid + r * FP_T;
+            if (j < M && s_st[j] == ST_UNDECIDED) und |= 1u << r;
+        }
         for (int gi = 0; gi <= M; ++gi) {
-            bool pending = false;
             for (int lr = 0; lr <= M; ++lr) {
                 bool progress = false;
-                pending = false;
+                /* every listed neighbour's state first (independent LDS reads),
+                 * then the decisions */
+                uint32_t kill = 0u, block = 0u;
 #pragma unroll
                 for (int r = 0; r < FP_R; ++r) {
+                    if (!((und >> r) & 1u) || nbc[r] < 0) continue;
                     const int j = tid + r * FP_T;
-                    if (j >= M || ld_state(&s_st[j]) != ST_UNDECIDED) continue;
-                    bool killed = false, blocked = false;
-                    if (nbc[r] >= 0) {
-                        for (int q = 0; q < nbc[r]; ++q) {
-                            const int k = (int)((nb[r][q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
+#pragma unroll
+                    for (int q = 0; q < FP_NB; ++q) {
+                        if (q < nbc[r]) {
+                            const int k = j + (int)(int8_t)((nb[r][q >> 2] >> (8 * (q & 3))) & 0xFFu);
                             const uint8_t st = ld_state(&s_st[k]);
-                            killed |= st == ST_KEPT;
-                            blocked |= st == ST_UNDECIDED;
+                            kill |= (st == ST_KEPT ? 1u : 0u) << r;
+                            block |= (st == ST_UNDECIDED ? 1u : 0u) << r;
                         }
-                    } else {
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < FP_R; ++r) {
+                    if (!((und >> r) & 1u)) continue;
+                    const int j = tid + r * FP_T;
+                    bool killed = (kill >> r) & 1u, blocked = (block >> r) & 1u;
+                    if (nbc[r] < 0) {                         /* more than FP_NB: scan */
                         const int64_t pj = s_mp[j];
                         const double vj = s_mh[j];
                         for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k) {
@@ -872,13 +890,15 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
                             }
                         }
                     }
-                    if (killed) { st_state(&s_st[j], ST_REMOVED); progress = true; }
-                    else if (!blocked) { st_state(&s_st[j], ST_KEPT); progress = true; }
-                    else pending = true;
+                    if (killed || !blocked) {
+                        st_state(&s_st[j], killed ? ST_REMOVED : ST_KEPT);
+                        und &= ~(1u << r);
+                        progress = true;
+                    }
                 }
                 if (!__ballot(progress)) break;                  /* wave-uniform */
             }
-            if (!__syncthreads_or(pending)) break;
+            if (!__syncthreads_or(und != 0u)) break;
         }
     }
     STAMP(3);
@@ -920,25 +940,47 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
             if (s_st[j] != ST_KEPT) continue;
             const double hj = s_mh[j];
             double lmin = INF, rmin = INF;
-            /* left: at k, the largest aligned block ending at k with no higher maximum */
-            for (int k = j - 1;;) {
-                if (k < 0) { lmin = fmin(lmin, s_vv[0]); break; }
-                if ((k & 511) == 511 && bh3[k >> 9] <= hj) { lmin = fmin(lmin, s_bvl[FL_B1 + FL_B2 + (k >> 9)]); k -= 512; continue; }
-                if ((k & 63) == 63 && bh2[k >> 6] <= hj) { lmin = fmin(lmin, s_bvl[FL_B1 + (k >> 6)]); k -= 64; continue; }
-                if ((k & 7) == 7 && s_bh[k >> 3] <= hj) { lmin = fmin(lmin, s_bvl[k >> 3]); k -= 8; continue; }
-                lmin = fmin(lmin, s_vv[k + 1]);
-                if (s_mh[k] > hj) break;
-                --k;
-            }
-            /* right: the largest aligned full block starting at k with no higher maximum */
-            for (int k = j + 1;;) {
-                if (k >= M) { rmin = fmin(rmin, s_vv[M]); break; }
-                if ((k & 511) == 0 && k + 511 < M && bh3[k >> 9] <= hj) { rmin = fmin(rmin, s_bvr[FL_B1 + FL_B2 + (k >> 9)]); k += 512; continue; }
-                if ((k & 63) == 0 && k + 63 < M && bh2[k >> 6] <= hj) { rmin = fmin(rmin, s_bvr[FL_B1 + (k >> 6)]); k += 64; continue; }
-                if ((k & 7) == 0 && k + 7 < M && s_bh[k >> 3] <= hj) { rmin = fmin(rmin, s_bvr[k >> 3]); k += 8; continue; }
-                rmin = fmin(rmin, s_vv[k]);
-                if (s_mh[k] > hj) break;
-                ++k;
+            /* the two walks step together, and a step reads every candidate
+             * (block maxima and valley minima of the 512-, 64- and 8-maximum
+             * blocks, the gap valley, the maximum) before choosing, so one LDS
+             * round trip covers a step of both sides.  Left: at k, the largest
+             * aligned block ending at k with no higher maximum; right: the
+             * largest aligned full block starting at k. */
+            int kl = j - 1, kr = j + 1;
+            bool dl = false, dr = false;
+            while (!(dl && dr)) {
+                if (!dl) {
+                    if (kl < 0) {
+                        lmin = fmin(lmin, s_vv[0]);
+                        dl = true;
+                    } else {
+                        const double b3 = bh3[kl >> 9], b2 = bh2[kl >> 6], b1 = s_bh[kl >> 3];
+                        const double v3 = s_bvl[FL_B1 + FL_B2 + (kl >> 9)], v2 = s_bvl[FL_B1 + (kl >> 6)];
+                        const double v1 = s_bvl[kl >> 3], vv = s_vv[kl + 1], mh = s_mh[kl];
+                        const bool c3 = (kl & 511) == 511 && b3 <= hj;
+                        const bool c2 = !c3 && (kl & 63) == 63 && b2 <= hj;
+                        const bool c1 = !c3 && !c2 && (kl & 7) == 7 && b1 <= hj;
+                        lmin = fmin(lmin, c3 ? v3 : (c2 ? v2 : (c1 ? v1 : vv)));
+                        if (!(c3 || c2 || c1) && mh > hj) dl = true;
+                        else kl -= c3 ? 512 : (c2 ? 64 : (c1 ? 8 : 1));
+                    }
+                }
+                if (!dr) {
+                    if (kr >= M) {
+                        rmin = fmin(rmin, s_vv[M]);
+                        dr = true;
+                    } else {
+                        const double b3 = bh3[kr >> 9], b2 = bh2[kr >> 6], b1 = s_bh[kr >> 3];
+                        const double v3 = s_bvr[FL_B1 + FL_B2 + (kr >> 9)], v2 = s_bvr[FL_B1 + (kr >> 6)];
+                        const double v1 = s_bvr[kr >> 3], vv = s_vv[kr], mh = s_mh[kr];
+                        const bool c3 = (kr & 511) == 0 && kr + 511 < M && b3 <= hj;
+                        const bool c2 = !c3 && (kr & 63) == 0 && kr + 63 < M && b2 <= hj;
+                        const bool c1 = !c3 && !c2 && (kr & 7) == 0 && kr + 7 < M && b1 <= hj;
+                        rmin = fmin(rmin, c3 ? v3 : (c2 ? v2 : (c1 ? v1 : vv)));
+                        if (!(c3 || c2 || c1) && mh > hj) dr = true;
+                        else kr += c3 ? 512 : (c2 ? 64 : (c1 ? 8 : 1));
+                    }
+                }
             }
             const double prom = hj - fmax(lmin, rmin);
             st_state(&s_st[j], thr <= prom ? ST_FINAL : ST_REMOVED);

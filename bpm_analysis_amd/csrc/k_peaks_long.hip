@@ -113,6 +113,7 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_place(PeakArgs A, FplArgs L) {
     }
     if (tid == 0) {
         L.mtot[f] = run;
+        if (L.dfail) L.dfail[f] = 0;
         double *vv = L.vv + d0 + f;
         if (n > 0) {
             vv[0] = A.sign * A.env[d0];
@@ -201,6 +202,7 @@ __global__ __launch_bounds__(1024) void k_fpl_distance(PeakArgs A, FplArgs L) {
     }
     const int64_t dist = A.distance;
     if (dist <= 1) return;
+    if (L.dchunk && !L.dfail[f]) return;                     /* k_fpl_dist_ch decided every chunk */
     if (M <= FPD_MMAX) {
         /* States in LDS and each candidate's higher-priority neighbours listed
          * once (up to four, as signed index offsets packed in a register; more
@@ -312,6 +314,136 @@ __global__ __launch_bounds__(1024) void k_fpl_distance(PeakArgs A, FplArgs L) {
         __syncthreads();
         if (!again) break;
     }
+}
+
+
+/* One workgroup per chunk of a long recording's maxima: nominal [c S, c S + S),
+ * taken from its first component start (a maximum >= distance after the
+ * previous one, or the first) to the first component start at or after the
+ * nominal end.  Components never straddle such a cut, so every chunk decides
+ * its own exactly as the whole-recording rounds would; a component reaching
+ * more than FPC_H maxima past the nominal end sets dfail and k_fpl_distance
+ * runs the recording's rounds (from whatever other chunks have decided: their
+ * decisions are final).  Rounds as k_find_peaks_lds: neighbour lists of up to
+ * eight 8-bit offsets, every listed state read before the decisions, rounds
+ * wave-locally, one barrier to cross waves. */
+__global__ __launch_bounds__(FPC_T) void k_fpl_dist_ch(PeakArgs A, FplArgs L) {
+    const int f = blockIdx.y;
+    if (!fpl_selected(A, f)) return;
+    const int64_t dist = A.distance;
+    if (dist <= 1) return;
+    const int M = L.mtot[f];
+    const int n0 = blockIdx.x * FPC_S;
+    if (n0 >= M) return;
+    const int tid = threadIdx.x;
+    const int64_t d0 = A.doff[f];
+    const int32_t *mp = L.mp + d0;
+    const double *mh = L.mh + d0;
+    uint8_t *st = A.state + d0;
+    __shared__ int s_js, s_je;
+    __shared__ int32_t s_mp[FPC_S + FPC_H];
+    __shared__ double s_mh[FPC_S + FPC_H];
+    __shared__ uint8_t s_st[FPC_S + FPC_H];
+    const int n1 = min(M, n0 + FPC_S), n2 = min(M, n1 + FPC_H);
+    if (tid == 0) { s_js = n1; s_je = n1 < M ? INT_MAX : M; }
+    __syncthreads();
+    auto is_start = [&](int j) { return j == 0 || (int64_t)mp[j] - (int64_t)mp[j - 1] >= dist; };
+    for (int j = n0 + tid; j < n1; j += FPC_T)
+        if (is_start(j)) atomicMin(&s_js, j);
+    if (n1 < M)
+        for (int j = n1 + tid; j < n2; j += FPC_T)
+            if (is_start(j)) atomicMin(&s_je, j);
+    __syncthreads();
+    const int js = s_js, je = s_je;
+    if (js >= n1) return;                                    /* no component starts here */
+    if (je == INT_MAX) {                                     /* a component runs past the halo */
+        if (tid == 0) __hip_atomic_store(&L.dfail[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int m = je - js;
+    for (int t = tid; t < m; t += FPC_T) {
+        s_mp[t] = mp[js + t];
+        s_mh[t] = mh[js + t];
+        s_st[t] = st[js + t];
+    }
+    __syncthreads();
+    constexpr int NBX = 8;
+    uint32_t nb[FPC_R][2];
+    int nbc[FPC_R];
+    uint32_t und = 0u;
+#pragma unroll
+    for (int r = 0; r < FPC_R; ++r) {
+        const int j = tid + r * FPC_T;
+        nb[r][0] = nb[r][1] = 0u;
+        nbc[r] = 0;
+        if (j >= m || s_st[j] != ST_UNDECIDED) continue;
+        und |= 1u << r;
+        const int64_t pj = s_mp[j];
+        const double vj = s_mh[j];
+        int c = 0;
+        auto add = [&](int k) {
+            const int o = k - j;
+            if (o < -128 || o > 127) c = NBX;
+            if (c < NBX) nb[r][c >> 2] |= ((uint32_t)o & 0xFFu) << (8 * (c & 3));
+            ++c;
+        };
+        for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k)
+            if (s_mh[k] > vj && s_st[k] == ST_UNDECIDED) add(k);       /* earlier index: strictly higher */
+        for (int k = j + 1; k < m && s_mp[k] - pj < dist; ++k)
+            if (s_mh[k] >= vj && s_st[k] == ST_UNDECIDED) add(k);      /* later index wins ties */
+        nbc[r] = c <= NBX ? c : -1;
+    }
+    for (int gi = 0; gi <= m; ++gi) {
+        for (int lr = 0; lr <= m; ++lr) {
+            bool progress = false;
+            uint32_t kill = 0u, block = 0u;
+#pragma unroll
+            for (int r = 0; r < FPC_R; ++r) {
+                if (!((und >> r) & 1u) || nbc[r] < 0) continue;
+                const int j = tid + r * FPC_T;
+#pragma unroll
+                for (int q = 0; q < NBX; ++q) {
+                    if (q < nbc[r]) {
+                        const int k = j + (int)(int8_t)((nb[r][q >> 2] >> (8 * (q & 3))) & 0xFFu);
+                        const uint8_t sk = ld_state(&s_st[k]);
+                        kill |= (sk == ST_KEPT ? 1u : 0u) << r;
+                        block |= (sk == ST_UNDECIDED ? 1u : 0u) << r;
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < FPC_R; ++r) {
+                if (!((und >> r) & 1u)) continue;
+                const int j = tid + r * FPC_T;
+                bool killed = (kill >> r) & 1u, blocked = (block >> r) & 1u;
+                if (nbc[r] < 0) {
+                    const int64_t pj = s_mp[j];
+                    const double vj = s_mh[j];
+                    for (int k = j - 1; k >= 0 && pj - s_mp[k] < dist; --k)
+                        if (s_mh[k] > vj) {
+                            const uint8_t sk = ld_state(&s_st[k]);
+                            if (sk == ST_KEPT) { killed = true; break; }
+                            if (sk == ST_UNDECIDED) blocked = true;
+                        }
+                    if (!killed)
+                        for (int k = j + 1; k < m && s_mp[k] - pj < dist; ++k)
+                            if (s_mh[k] >= vj) {
+                                const uint8_t sk = ld_state(&s_st[k]);
+                                if (sk == ST_KEPT) { killed = true; break; }
+                                if (sk == ST_UNDECIDED) blocked = true;
+                            }
+                }
+                if (killed || !blocked) {
+                    st_state(&s_st[j], killed ? ST_REMOVED : ST_KEPT);
+                    und &= ~(1u << r);
+                    progress = true;
+                }
+            }
+            if (!__ballot(progress)) break;
+        }
+        if (!__syncthreads_or(und != 0u)) break;
+    }
+    for (int t = tid; t < m; t += FPC_T) st[js + t] = s_st[t];
 }
 
 __global__ __launch_bounds__(FPL_T) void k_fpl_prom(PeakArgs A, FplArgs L) {

@@ -366,6 +366,9 @@ def test_find_peaks_kernels_agree(det):
         np.concatenate([np.full(70_000, 5.0), 300 * beat[:70_000] + 20]),    # flat head: edge gaps
         np.round(rng.random(m) * 3) + 200 * (t % 700 == 0),                 # plateaus and ties everywhere
         300 * beat[:66_000] + rng.random(66_000),
+        # sparse maxima (k_fpl_dist_ch cuts them into chunks) then dense noise
+        # (one component past the chunk halo: k_fpl_distance finishes the rest)
+        np.concatenate([300 * beat[:100_000] + 20, rng.random(100_000) * 10 + 5]),
     ]
     envs2 = long_envs + envs[-3:]
     a = det.run_env_host(envs2, 302, params, stages)
