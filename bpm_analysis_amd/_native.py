@@ -33,6 +33,7 @@ OPT_HILBERT_R2C = 512
 OPT_REF_SERIAL_MEAN = 1024
 OPT_STATS = 2048
 OPT_HILBERT_BLUESTEIN = 4096
+OPT_REF_NOSPLIT = 8192
 STAT_RAW_TROUGHS, STAT_UNDECIDED, STAT_FULL_DRAFT, NSTATS = 0, 1, 2, 8
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 

@@ -353,13 +353,55 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             const bool zb = P->ba_b[1] == 0.0 && P->ba_b[3] == 0.0 && P->ba_b[4] == P->ba_b[0] &&
                             P->ba_b[2] == -2.0 * P->ba_b[0] &&
                             (P->dtype == BPMX_DT_U8 || P->dtype == BPMX_DT_I16 || P->dtype == BPMX_DT_I32);
-#define ENV_REF_K(DT, M, Z) LAUNCH(ctx, s, "k_envelope_ref", (k_envelope_ref_t<DT, M, Z>), g, b, 0, s, a)
+            /* the forward pass in row chunks while k_ref_pick gathers the next
+             * chunks on a side stream (BPMX_OPT_REF_NOSPLIT: one gather, then
+             * the whole pass in k_envelope_ref_t) */
+            const int64_t rows = maxnd + 30;
+            /* chunk k: rows [R (2^k - 1), R (2^(k+1) - 1)): the first gather is
+             * short (it is not overlapped), the later ones grow while the
+             * gather (faster per row than the sequential pass) stays ahead */
+            auto fwd_row = [&](int64_t k) -> int64_t { return std::min(rows, REF_FWD_ROWS * ((int64_t(1) << k) - 1)); };
+            int64_t nfc = 1;
+            while (fwd_row(nfc) < rows) ++nfc;
+            const bool split = nfc >= 2 && !(P->options & BPMX_OPT_REF_NOSPLIT) && ctx->side_ready() &&
+                               ctx->ref_events((size_t)nfc);
+            a.pick_r0 = 0; a.fwd_rb = 0; a.fwd_re = 0; a.fwd_z = nullptr;
+            if (split) {
+                a.fwd_z = (double *)ctx->buf("ref_fwd_z", (size_t)F * 4 * 8, &rc);
+                if (rc != BPMX_OK) return rc;
+            }
+            auto env_ref = [&](void (*pick)(EnvRefArgs), void (*body)(EnvRefArgs), void (*fwd)(EnvRefArgs)) -> int {
+                if (!split) {
+                    LAUNCH(ctx, s, "k_ref_pick", pick, gp, dim3(256), 0, s, a);
+                    LAUNCH(ctx, s, "k_envelope_ref", body, g, b, 0, s, a);
+                    return BPMX_OK;
+                }
+                EnvRefArgs c = a;
+                hipStream_t s2 = ctx->side[0];
+                HIP_TRY(hipEventRecord(ctx->side_fork, s));
+                HIP_TRY(hipStreamWaitEvent(s2, ctx->side_fork, 0));
+                for (int64_t k = 0; k < nfc; ++k) {
+                    const int64_t r0 = fwd_row(k), r1 = fwd_row(k + 1);
+                    c.pick_r0 = r0;
+                    const dim3 gk((unsigned)((r1 - r0 + 63) / 64), (unsigned)((F + 63) / 64));
+                    hipStream_t sk = k == 0 ? s : s2;
+                    LAUNCH(ctx, sk, "k_ref_pick", pick, gk, dim3(256), 0, sk, c);
+                    if (k > 0) HIP_TRY(hipEventRecord(ctx->ref_ev[k], s2));
+                }
+                for (int64_t k = 0; k < nfc; ++k) {
+                    if (k > 0) HIP_TRY(hipStreamWaitEvent(s, ctx->ref_ev[k], 0));
+                    c.fwd_rb = fwd_row(k);
+                    c.fwd_re = fwd_row(k + 1);
+                    LAUNCH(ctx, s, "k_ref_fwd", fwd, g, b, 0, s, c);
+                }
+                LAUNCH(ctx, s, "k_envelope_ref", body, g, b, 0, s, c);
+                return BPMX_OK;
+            };
+#define ENV_REF_K(DT, M, Z) rc = env_ref(k_ref_pick<DT, M>, k_envelope_ref_t<DT, M, Z>, k_ref_fwd<Z>)
 #define ENV_REF(DT)                                                                                  \
     if (multi) {                                                                                     \
-        LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, true>), gp, dim3(256), 0, s, a);                 \
         if (zb && DT <= BPMX_DT_I32) ENV_REF_K(DT, true, DT <= BPMX_DT_I32); else ENV_REF_K(DT, true, false); \
     } else {                                                                                         \
-        LAUNCH(ctx, s, "k_ref_pick", (k_ref_pick<DT, false>), gp, dim3(256), 0, s, a);                \
         if (zb && DT <= BPMX_DT_I32) ENV_REF_K(DT, false, DT <= BPMX_DT_I32); else ENV_REF_K(DT, false, false); \
     }
             switch (P->dtype) {
@@ -369,6 +411,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             case BPMX_DT_F32: ENV_REF(BPMX_DT_F32) break;
             default: ENV_REF(BPMX_DT_F64) break;
             }
+            if (rc != BPMX_OK) return rc;
 #undef ENV_REF
 #undef ENV_REF_K
             if (chain)
@@ -681,7 +724,11 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
             const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);
+            a.vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 8, &rc);
+            if (rc != BPMX_OK) return rc;
             LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
+            const unsigned gp = (unsigned)std::max<int64_t>(1, (trmax + DP_CHUNK - 1) / DP_CHUNK);
+            LAUNCH(ctx, s, "k_draft_points", k_draft_points, dim3(F, gp), dim3(DB_T), 0, s, a);
         }
         if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {

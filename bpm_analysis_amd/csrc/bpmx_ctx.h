@@ -60,6 +60,15 @@ struct bpmx_ctx {
     static constexpr int NSIDE = 4;
     hipStream_t side[NSIDE] = {};
     hipEvent_t side_fork = nullptr, side_join[NSIDE] = {};
+    std::vector<hipEvent_t> ref_ev;   /* reference mode: row chunk k gathered (side stream) */
+    bool ref_events(size_t n) {
+        while (ref_ev.size() < n) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+            ref_ev.push_back(e);
+        }
+        return true;
+    }
     bool side_ready() {
         if (side[0]) return true;
         for (int i = 0; i < NSIDE; ++i) {

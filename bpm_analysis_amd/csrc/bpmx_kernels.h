@@ -23,11 +23,20 @@ struct EnvRefArgs {
     double *y;             /* [sumNd] or null */
     double *sums;          /* interleaved [maxNd * F]: the rolling sum after each step (chain mode), or null */
     int32_t *chain;        /* [F]: 1 = env left to k_ref_env_mean (chain mode), 0 = written in the pass */
+    int64_t pick_r0;       /* k_ref_pick: first row of this launch's rows */
+    /* split forward pass (k_ref_fwd over row chunks while later chunks are
+     * picked on a side stream): rows [fwd_rb, fwd_re) and the DF2T state
+     * [F][4] between chunks; fwd_z null: k_envelope_ref_t runs the forward pass */
+    int64_t fwd_rb, fwd_re;
+    double *fwd_z;
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
 };
 __global__ void k_ref_env_mean(EnvRefArgs A);
+template <bool ZB>
+__global__ void k_ref_fwd(EnvRefArgs A);
+constexpr int64_t REF_FWD_ROWS = 1024;   /* first forward chunk's rows, doubling per chunk (multiples of the prefetch block) */
 
 struct QuantArgs {
     const double *env;
@@ -229,7 +238,11 @@ struct DraftBoundArgs {
     int32_t local_m;         /* more troughs than this: rank segments per window (DB_LOCAL_M) */
     int64_t *stats;          /* optional (BPMX_OPT_STATS): += raw troughs, undecided troughs, chunks sent to the
                                 full draft by draft_point */
+    int32_t *vfl;            /* [F][2] k_draft_bounds out: first / last valid draft output (k_draft_points) */
 };
+/* k_draft_points: the undecided troughs of DP_CHUNK consecutive raw troughs per
+ * workgroup, one wave per trough */
+constexpr int DP_CHUNK = 32;
 constexpr int DB_T = 256;
 constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */
 constexpr int DB_LOCAL_M = 512;  /* more troughs than this: per-window ranking instead of the global order */
@@ -270,6 +283,7 @@ __global__ void k_find_peaks_lds(PeakArgs A);
 __global__ void k_interp(InterpArgs A);
 __global__ void k_sanitize(SanitizeArgs A);
 __global__ void k_draft_bounds(DraftBoundArgs A);
+__global__ void k_draft_points(DraftBoundArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>
 __global__ void k_rolling_quantile(RollqArgs A);

@@ -192,7 +192,7 @@ template <int DT, bool MULTI>
 __global__ __launch_bounds__(256) void k_ref_pick(EnvRefArgs A) {
     __shared__ double tile[64][65];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t r0 = (int64_t)blockIdx.x * 64, f0 = (int64_t)blockIdx.y * 64;
+    const int64_t r0 = A.pick_r0 + (int64_t)blockIdx.x * 64, f0 = (int64_t)blockIdx.y * 64;
     const int64_t S = A.n_files, ds = A.ds;
     const int ch = A.channels, wdt = work_dtype(DT, MULTI ? 2 : 1);
     for (int fi = wv; fi < 64; fi += 4) {
@@ -306,6 +306,73 @@ __device__ __forceinline__ void kahan_chain(RollMean &R, const double *__restric
     }
 }
 
+
+/* The forward pass alone over rows [fwd_rb, fwd_re) (a multiple of PFB), the
+ * DF2T state carried between launches in fwd_z: the host runs it chunk by chunk
+ * while k_ref_pick gathers the next chunks on a side stream, so the gather
+ * (HBM sector bound, many waves) overlaps the sequential pass (16 waves). */
+template <bool ZB>
+__global__ __launch_bounds__(64) void k_ref_fwd(EnvRefArgs A) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x * 64 + lane;
+    const bool have = f < A.n_files;
+    int64_t nd = have ? A.doff[f + 1] - A.doff[f] : 0;
+    const bool run = have && nd > 15 && A.active[f];
+    if (!run) nd = 0;
+    const int64_t S = A.n_files;
+    double *__restrict__ scr = A.scratch + (have ? f : 0);
+    int64_t ndmax = nd;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmax, o); ndmax = t > ndmax ? t : ndmax; }
+    if (ndmax == 0) return;
+    int64_t ndmin = run ? nd : INT64_MAX;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmin, o); ndmin = t < ndmin ? t : ndmin; }
+    Df2t D;
+    D.b0 = A.b[0]; D.b1 = A.b[1]; D.b2 = A.b[2]; D.b3 = A.b[3]; D.b4 = A.b[4];
+    D.a1 = A.a[1]; D.a2 = A.a[2]; D.a3 = A.a[3]; D.a4 = A.a[4];
+    const int64_t SB = (int64_t)PFB * S;
+    const int64_t nemax = ndmax + 30;
+    const int64_t ne = run ? nd + 30 : nemax;
+    const int64_t nemin = ndmin == INT64_MAX ? nemax : ndmin + 30;
+    const int64_t rb = A.fwd_rb, re = A.fwd_re < nemax ? A.fwd_re : nemax;
+    if (rb >= re) return;
+    auto ldc = [&](int64_t r) -> double { return scr[(r < ne ? r : ne - 1) * S]; };
+    double cur[PFB], nxt[PFB];
+#pragma unroll
+    for (int u = 0; u < PFB; ++u) cur[u] = ldc(rb + u);
+    double *zs = A.fwd_z + (have ? (int64_t)f * 4 : 0);
+    if (run) {
+        if (rb == 0) D.init(A.zi, cur[0]);
+        else { D.z0 = zs[0]; D.z1 = zs[1]; D.z2 = zs[2]; D.z3 = zs[3]; }
+    }
+    double *p = scr + rb * S;
+    for (int64_t r0 = rb; r0 < re; r0 += PFB, p += SB) {
+        /* the next block: rows past re may not be gathered yet; they are
+         * read but never used (the next launch loads its own first block) */
+        if (r0 + 2 * PFB <= nemin) {
+#pragma unroll
+            for (int u = 0; u < PFB; ++u) nxt[u] = p[SB + u * S];
+        } else {
+#pragma unroll
+            for (int u = 0; u < PFB; ++u) nxt[u] = ldc(r0 + PFB + u);
+        }
+        if (r0 + PFB <= nemin) {
+            if (run) {
+#pragma unroll
+                for (int u = 0; u < PFB; ++u) p[u * S] = D.step<ZB>(cur[u]);
+            }
+        } else if (run) {
+#pragma unroll
+            for (int u = 0; u < PFB; ++u)
+                if (r0 + u < ne) p[u * S] = D.step<ZB>(cur[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < PFB; ++u) cur[u] = nxt[u];
+    }
+    if (run) { zs[0] = D.z0; zs[1] = D.z1; zs[2] = D.z2; zs[3] = D.z3; }
+}
+template __global__ void k_ref_fwd<false>(EnvRefArgs);
+template __global__ void k_ref_fwd<true>(EnvRefArgs);
+
 template <int DT, bool MULTI, bool ZB>
 __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     __shared__ double st_env[STG][65];
@@ -347,7 +414,7 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
     const int64_t ne = run ? nd + 30 : nemax;
     const int64_t nemin = ndmin == INT64_MAX ? nemax : ndmin + 30;   /* shortest running column */
     /* ---------------- forward pass, in place over the gathered rows ---------------- */
-    {
+    if (!A.fwd_z) {                                          /* else k_ref_fwd ran it in row chunks */
         auto ldc = [&](int64_t r) -> double { return scr[(r < ne ? r : ne - 1) * S]; };   /* clamped */
         double cur[PFB], nxt[PFB];
 #pragma unroll

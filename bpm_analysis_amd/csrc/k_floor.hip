@@ -707,21 +707,24 @@ __device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int64_t lo, in
  * element above it (one more binary search position per segment).  Returns
  * false for what it does not take (more than 64 DP_SPL segments, non-finite
  * trough values): the recording then gets the full draft. */
-constexpr int DP_SPL = 4;
+constexpr int DP_SPL_MAX = 4;
+constexpr int DP_IP_ROUNDS = 8;
+constexpr int DP_FIX = 4;         /* exact steps after a segment's inverse estimate before bisection */   /* interpolated value pivots before random element pivots */
 
+template <int DP_SPL>
 __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s_tv, int base, int m, int64_t n,
                                             int64_t lo, int64_t hi, int jl, int jh, double q, uint32_t seed,
                                             double *res) {
     const int lane = lane_id();
     if (jh - jl + 1 > 64 * DP_SPL) return false;
     int32_t sa[DP_SPL], sn[DP_SPL], st[DP_SPL], slo[DP_SPL], shi[DP_SPL], sub[DP_SPL];
-    double sy[DP_SPL], ssl[DP_SPL];
+    double sy[DP_SPL], ssl[DP_SPL], sinv[DP_SPL];
     bool sinc[DP_SPL], scst[DP_SPL];
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < DP_SPL; ++r) {
         const int i = jl + lane + 64 * r;
-        sn[r] = 0; sa[r] = 0; st[r] = 0; sy[r] = 0.0; ssl[r] = 0.0; sinc[r] = true; scst[r] = true;
+        sn[r] = 0; sa[r] = 0; st[r] = 0; sy[r] = 0.0; ssl[r] = 0.0; sinv[r] = 0.0; sinc[r] = true; scst[r] = true;
         if (i <= jh) {
             const int64_t tj = s_tp[i - base];
             const int64_t nx = i + 1 < m ? (int64_t)s_tp[i + 1 - base] : n;
@@ -736,6 +739,7 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             ok = ok && __builtin_isfinite(y0) && __builtin_isfinite(y1) && __builtin_isfinite(sl);
             sa[r] = (int32_t)a; sn[r] = (int32_t)(b - a); st[r] = (int32_t)tj;
             sy[r] = y0; ssl[r] = sl; sinc[r] = y1 >= y0;
+            sinv[r] = sl != 0.0 ? 1.0 / sl : 0.0;
         }
         slo[r] = 0; shi[r] = sn[r]; sub[r] = 0;
     }
@@ -764,32 +768,133 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
         const int incl = wave_iscan_dpp<false>(cnt);
         const int tot = __shfl(incl, 63);
         if (tot <= 0) return false;
-        rng = rng * 1664525u + 1013904223u;
-        const int p = (int)(((uint64_t)rng * (uint64_t)tot) >> 32);
         const int excl = incl - cnt;
-        const bool own = p >= excl && p < incl;
-        const int owner = __ffsll((unsigned long long)__ballot(own)) - 1;
-        double pvl = 0.0;
-        if (own) {
-            int off = p - excl;
+        if (DP_SPL == 1 && tot <= 64) {
+            /* few left: lane o takes the active element at offset o (its
+             * segment's parameters fetched from the owning lane), a bitonic
+             * sort across the wave, then the (k - below)-th and the next */
+            const int o = lane;
+            int s = 0;                                       /* owner: last lane with excl <= o */
 #pragma unroll
-            for (int r = 0; r < DP_SPL; ++r) {
-                const int c = shi[r] - slo[r];
-                if (off >= 0 && off < c) pvl = sorted(r, slo[r] + off);
-                off -= c;
+            for (int b = 32; b > 0; b >>= 1) {
+                const int ex = __shfl(excl, s + b - 1 + 1 > 63 ? 63 : s + b);
+                if (s + b <= 63 && ex <= o) s += b;
             }
+            const int exs = __shfl(excl, s), los = __shfl(slo[0], s), sas = __shfl(sa[0], s), sns = __shfl(sn[0], s);
+            const int sts = __shfl(st[0], s);
+            const double sys = __shfl(sy[0], s), ssls = __shfl(ssl[0], s);
+            const bool incs = __shfl((int)sinc[0], s) != 0, csts = __shfl((int)scst[0], s) != 0;
+            double x = __builtin_inf();
+            if (o < tot) {
+                const int i = los + (o - exs);
+                const int64_t xp = incs ? (int64_t)sas + i : (int64_t)sas + sns - 1 - i;
+                x = (csts || xp == sts) ? sys : ssls * ((double)xp - (double)sts) + sys;
+            }
+#pragma unroll
+            for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+                for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                    const double y = __shfl_xor(x, jj);
+                    const bool up = (lane & kk) == 0, lower = (lane & jj) == 0;
+                    x = (lower == up) ? fmin(x, y) : fmax(x, y);
+                }
+            }
+            const int t = (int)(k - below);
+            va = __shfl(x, t);
+            if (!interp) {
+                *res = va;
+                return true;
+            }
+            double vb;
+            if (t + 1 < tot) {
+                vb = __shfl(x, t + 1);
+            } else {                                         /* the least element above the active ones */
+                const double mn = shi[0] < sn[0] ? sorted(0, shi[0]) : __builtin_inf();
+                vb = wave_min(mn);
+            }
+            *res = va + (vb - va) * (idxf - (double)k);
+            return true;
         }
-        const double pv = __shfl(pvl, owner);
+        double pv;
+        if (it < DP_IP_ROUNDS) {
+            /* a value pivot interpolated between the active extremes at the
+             * target's rank: the values within a segment are evenly spaced, so
+             * the active set shrinks by far more than a random pivot's half */
+            double amin = __builtin_inf(), amax = -__builtin_inf();
+#pragma unroll
+            for (int r = 0; r < DP_SPL; ++r)
+                if (shi[r] > slo[r]) { amin = fmin(amin, sorted(r, slo[r])); amax = fmax(amax, sorted(r, shi[r] - 1)); }
+            amin = wave_min(amin);
+            amax = wave_max(amax);
+            if (!(amin < amax)) {                            /* every active element is equal */
+                va = amin;
+                leq = below + tot;
+#pragma unroll
+                for (int r = 0; r < DP_SPL; ++r) sub[r] = shi[r];   /* beyond: larger values only */
+                break;
+            }
+            pv = amin + (amax - amin) * (((double)(k - below) + 0.5) / (double)tot);
+            pv = fmin(fmax(pv, amin), amax);
+        } else {
+            rng = rng * 1664525u + 1013904223u;
+            const int p = (int)(((uint64_t)rng * (uint64_t)tot) >> 32);
+            const bool own = p >= excl && p < incl;
+            const int owner = __ffsll((unsigned long long)__ballot(own)) - 1;
+            double pvl = 0.0;
+            if (own) {
+                int off = p - excl;
+#pragma unroll
+                for (int r = 0; r < DP_SPL; ++r) {
+                    const int c = shi[r] - slo[r];
+                    if (off >= 0 && off < c) pvl = sorted(r, slo[r] + off);
+                    off -= c;
+                }
+            }
+            pv = __shfl(pvl, owner);
+        }
         int slb[DP_SPL];
         int cl = 0, ce = 0;
 #pragma unroll
         for (int r = 0; r < DP_SPL; ++r) {
-            int l = slo[r], h = shi[r];
-            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) < pv) l = mid + 1; else h = mid; }
-            slb[r] = l;
-            h = shi[r];
-            while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) <= pv) l = mid + 1; else h = mid; }
-            sub[r] = l;
+            /* first active rank with a value >= pv, then > pv: started from
+             * the segment formula's inverse (values evenly spaced) and made
+             * exact by stepping over at most DP_FIX neighbours; a search
+             * that needs more is finished by bisection */
+            const int l0 = slo[r], h0 = shi[r];
+            int i = l0;
+            if (l0 < h0) {
+                if (scst[r] || ssl[r] == 0.0) {
+                    i = sy[r] < pv ? h0 : l0;                /* every value is y0 */
+                } else {
+                    const double xf = (double)st[r] + (pv - sy[r]) * sinv[r];
+                    const double ie = sinc[r] ? ceil(xf) - (double)sa[r] : (double)(sa[r] + sn[r] - 1) - floor(xf);
+                    i = (int)fmin(fmax(ie, (double)l0), (double)h0);   /* NaN: l0 */
+                    int g = 0;
+                    while (i > l0 && g < DP_FIX && sorted(r, i - 1) >= pv) { --i; ++g; }
+                    while (i < h0 && g < DP_FIX && sorted(r, i) < pv) { ++i; ++g; }
+                    if (g >= DP_FIX) {
+                        int l = l0, h = h0;
+                        while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) < pv) l = mid + 1; else h = mid; }
+                        i = l;
+                    }
+                }
+            }
+            slb[r] = i;
+            int u = i;
+            if (u < h0) {
+                if (scst[r] || ssl[r] == 0.0) {
+                    u = sy[r] <= pv ? h0 : u;
+                } else {
+                    int g = 0;
+                    while (u < h0 && g < DP_FIX && sorted(r, u) <= pv) { ++u; ++g; }
+                    if (g >= DP_FIX) {
+                        int l = u, h = h0;
+                        while (l < h) { const int mid = (l + h) >> 1; if (sorted(r, mid) <= pv) l = mid + 1; else h = mid; }
+                        u = l;
+                    }
+                }
+            }
+            sub[r] = u;
             cl += slb[r] - slo[r];
             ce += sub[r] - slo[r];
         }
@@ -840,7 +945,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     } s_o;
     int16_t *s_olo = s_o.ord[0], *s_ohi = s_o.ord[1];
     DbSeg *s_slo = s_o.seg[0], *s_shi = s_o.seg[1];
-    __shared__ int s_vf, s_vl, s_undecided, s_nund;
+    __shared__ int s_vf, s_vl;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int m = A.nraw[f];
     const int tid = threadIdx.x;
@@ -860,7 +965,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
     const int64_t *raw = A.raw + d0;
     const double *env = A.env + d0;
     const int64_t W = A.window, t0 = raw[0], off = (W - 1) / 2;
-    if (tid == 0) { s_vf = INT_MAX; s_vl = -1; s_undecided = 0; s_nund = 0; }
+    if (tid == 0) { s_vf = INT_MAX; s_vl = -1; }
     __syncthreads();
     /* valid outputs (nobs >= min_periods) form one interval: with s >= t0 and
      * e <= n (outputs [t0 + W - 1 - off, n - 1 - off]) nobs = W >= min_periods,
@@ -959,7 +1064,6 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         while (lo < hi) { const int mid = (lo + hi) >> 1; if (tp(mid) <= x) lo = mid + 1; else hi = mid; }
         return lo - 1;
     };
-    bool any_undecided = false;
     for (int j = jc0 + tid; j < jc1; j += DB_T) {
         const int64_t t = tp(j);
         const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
@@ -1020,38 +1124,93 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         uint8_t dcs;
         if (et <= A.mult * L) dcs = 1;
         else if (et > A.mult * U * (1.0 + 0x1p-50)) dcs = 0;
-        else { dcs = 2; any_undecided = true; }
+        else dcs = 2;                                  /* k_draft_points */
         A.dec[d0 + j] = dcs;
     }
-    if (any_undecided) s_undecided = 1;
-    __syncthreads();
     if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)(jc1 - jc0));
-    if (!s_undecided) return;
-    /* Undecided troughs: the exact draft value at each, one wave per trough
-     * (draft_point) over the staged troughs, which cover every window of the
-     * chunk.  The segment records are no longer read: their LDS holds the list. */
-    int16_t *s_und = s_o.ord[0];
+    if (tid == 0 && blockIdx.y == 0) { A.vfl[2 * f] = vf; A.vfl[2 * f + 1] = vl; }
+}
+
+/* The troughs k_draft_bounds leaves undecided (dec 2): the exact draft value at
+ * each (draft_point), one wave per trough, DP_CHUNK consecutive raw troughs per
+ * workgroup, so a recording's undecided troughs spread over many waves.  A
+ * workgroup stages the troughs its windows reach.  A trough draft_point does
+ * not take sends the recording to the full draft (exact). */
+__global__ __launch_bounds__(DB_T) void k_draft_points(DraftBoundArgs A) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files || !A.run[f]) return;
+    const int m = A.nraw[f];
+    const int jc0 = (int)blockIdx.y * DP_CHUNK;
+    if (jc0 >= m) return;
+    const int jc1 = min(m, jc0 + DP_CHUNK);
+    const int tid = threadIdx.x;
+    const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
+    __shared__ int32_t s_tp[DB_TRMAX];
+    __shared__ double s_tv[DB_TRMAX];
+    __shared__ int16_t s_und[DP_CHUNK];
+    __shared__ int s_nund;
+    if (tid == 0) s_nund = 0;
+    __syncthreads();
     for (int j = jc0 + tid; j < jc1; j += DB_T)
         if (A.dec[d0 + j] == 2) s_und[atomicAdd(&s_nund, 1)] = (int16_t)(j - jc0);
     __syncthreads();
     const int nu = s_nund;
+    if (nu == 0) return;
+    if (__hip_atomic_load(&A.exact[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   /* full draft anyway */
+    const int64_t *raw = A.raw + d0;
+    const double *env = A.env + d0;
+    const int64_t W = A.window, t0 = raw[0];
+    const int vf = A.vfl[2 * f], vl = A.vfl[2 * f + 1];
+    auto seg_of_g = [&](int64_t x) -> int {                 /* last trough <= x, over global memory */
+        int lo = 0, hi = m;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (raw[mid] <= x) lo = mid + 1; else hi = mid; }
+        return lo - 1;
+    };
+    auto qpos = [&](int j) -> int64_t { const int64_t t = raw[j]; return t < vf ? vf : (t > vl ? vl : t); };
+    int64_t s, e;
+    win_bounds(qpos(jc0), n, W, s, e);
+    const int ja = seg_of_g(s > t0 ? s : t0);
+    win_bounds(qpos(jc1 - 1), n, W, s, e);
+    const int jb = seg_of_g(e - 1);
+    const int base = min(ja, jc0);
+    const int top = min(m - 1, max(jb + 1, jc1 - 1));
+    const int ns = top - base + 1;
+    if (ns > DB_TRMAX) {                                     /* windows too wide to stage */
+        if (tid == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    for (int j = tid; j < ns; j += DB_T) {
+        const int64_t t = raw[base + j];
+        s_tp[j] = (int32_t)t;
+        s_tv[j] = env[t];
+    }
+    __syncthreads();
+    auto seg_of = [&](int64_t x) -> int {                   /* last trough <= x (x >= t0), among the staged */
+        int lo = base, hi = base + ns;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_tp[mid - base] <= x) lo = mid + 1; else hi = mid; }
+        return lo - 1;
+    };
     bool fail = false;
     for (int u = wave_id(); u < nu; u += DB_T / 64) {
         const int j = jc0 + s_und[u];
-        const int64_t t = tp(j);
+        const int64_t t = s_tp[j - base];
         const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
-        int64_t s, e;
         win_bounds(qp, n, W, s, e);
         const int64_t lo = s > t0 ? s : t0, hi = e;
         double r = 0.0;
-        if (!draft_point(s_tp, s_tv, base, m, n, lo, hi, seg_of(lo), seg_of(hi - 1), A.q,
-                         0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu, &r)) {
+        /* one segment per lane when the window has <= 64 (the common case: a
+         * quarter of the per-round work of four per lane) */
+        const int jl = seg_of(lo), jh = seg_of(hi - 1);
+        const uint32_t seed = 0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu;
+        const bool ok = jh - jl + 1 <= 64 ? draft_point<1>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r)
+                                          : draft_point<DP_SPL_MAX>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r);
+        if (!ok) {
             fail = true;
             continue;
         }
-        if (lane_id() == 0) A.dec[d0 + j] = (r == r && tv(j) <= A.mult * r) ? 1 : 0;
+        if (lane_id() == 0) A.dec[d0 + j] = (r == r && s_tv[j - base] <= A.mult * r) ? 1 : 0;
     }
-    if (fail && lane_id() == 0) A.exact[f] = 1;          /* zeroed before the launch */
+    if (fail && lane_id() == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
     if (A.stats && fail && lane_id() == 0) atomicAdd((unsigned long long *)&A.stats[2], 1ull);
 }

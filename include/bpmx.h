@@ -96,8 +96,11 @@ enum bpmx_option {
     BPMX_OPT_REF_SERIAL_MEAN = 1024, /* reference mode: form the rolling mean's outputs inside the sequential
                                         pass instead of from its running sums in parallel (test/diagnostic) */
     BPMX_OPT_STATS = 2048,           /* count the run's path decisions for bpmx_stats (diagnostic) */
-    BPMX_OPT_HILBERT_BLUESTEIN = 4096 /* native mode, long recordings: rocFFT Bluestein instead of the exact-
+    BPMX_OPT_HILBERT_BLUESTEIN = 4096, /* native mode, long recordings: rocFFT Bluestein instead of the exact-
                                          length four-step transform (test/diagnostic) */
+    BPMX_OPT_REF_NOSPLIT = 8192      /* reference mode: gather every decimated sample first, then the forward
+                                        pass inside k_envelope_ref, instead of forward-pass row chunks
+                                        overlapping the next chunks' gather on a side stream (diagnostic) */
 };
 
 /* bpmx_stats counters of the last run with BPMX_OPT_STATS */
