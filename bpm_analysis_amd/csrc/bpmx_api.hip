@@ -728,7 +728,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             if (rc != BPMX_OK) return rc;
             LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
             const unsigned gp = (unsigned)std::max<int64_t>(1, (trmax + DP_CHUNK - 1) / DP_CHUNK);
-            LAUNCH(ctx, s, "k_draft_points", k_draft_points, dim3(F, gp), dim3(DB_T), 0, s, a);
+            LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
+            LAUNCH(ctx, s, "k_draft_points[wide]", k_draft_points<4>, dim3(F, gp), dim3(DB_T), 0, s, a);
         }
         if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
         {

@@ -283,6 +283,7 @@ __global__ void k_find_peaks_lds(PeakArgs A);
 __global__ void k_interp(InterpArgs A);
 __global__ void k_sanitize(SanitizeArgs A);
 __global__ void k_draft_bounds(DraftBoundArgs A);
+template <int SPL>
 __global__ void k_draft_points(DraftBoundArgs A);
 __global__ void k_floor_final(FinalArgs A);
 template <int T, int RQ_MAXCH>

@@ -708,6 +708,9 @@ __device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int64_t lo, in
  * false for what it does not take (more than 64 DP_SPL segments, non-finite
  * trough values): the recording then gets the full draft. */
 constexpr int DP_SPL_MAX = 4;
+#ifndef BPMX_DP_WAVES
+#define BPMX_DP_WAVES 6   /* waves per SIMD the one-segment k_draft_points is compiled for */
+#endif
 constexpr int DP_IP_ROUNDS = 8;
 constexpr int DP_FIX = 4;         /* exact steps after a segment's inverse estimate before bisection */   /* interpolated value pivots before random element pivots */
 
@@ -1136,7 +1139,8 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
  * workgroup, so a recording's undecided troughs spread over many waves.  A
  * workgroup stages the troughs its windows reach.  A trough draft_point does
  * not take sends the recording to the full draft (exact). */
-__global__ __launch_bounds__(DB_T) void k_draft_points(DraftBoundArgs A) {
+template <int SPL>
+__global__ __launch_bounds__(DB_T, SPL == 1 ? BPMX_DP_WAVES : 1) void k_draft_points(DraftBoundArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.run[f]) return;
     const int m = A.nraw[f];
@@ -1198,22 +1202,24 @@ __global__ __launch_bounds__(DB_T) void k_draft_points(DraftBoundArgs A) {
         win_bounds(qp, n, W, s, e);
         const int64_t lo = s > t0 ? s : t0, hi = e;
         double r = 0.0;
-        /* one segment per lane when the window has <= 64 (the common case: a
-         * quarter of the per-round work of four per lane) */
+        /* SPL 1: one segment per lane, windows of <= 64 segments (the common
+         * case); wider ones stay undecided for the SPL 4 launch, so the
+         * common kernel keeps the registers of one segment per lane */
         const int jl = seg_of(lo), jh = seg_of(hi - 1);
+        if (SPL == 1 && jh - jl + 1 > 64) continue;
         const uint32_t seed = 0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu;
-        const bool ok = jh - jl + 1 <= 64 ? draft_point<1>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r)
-                                          : draft_point<DP_SPL_MAX>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r);
-        if (!ok) {
+        if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r)) {
             fail = true;
             continue;
         }
         if (lane_id() == 0) A.dec[d0 + j] = (r == r && s_tv[j - base] <= A.mult * r) ? 1 : 0;
     }
     if (fail && lane_id() == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
+    if (A.stats && SPL == 1 && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
     if (A.stats && fail && lane_id() == 0) atomicAdd((unsigned long long *)&A.stats[2], 1ull);
 }
+template __global__ void k_draft_points<1>(DraftBoundArgs);
+template __global__ void k_draft_points<DP_SPL_MAX>(DraftBoundArgs);
 
 __global__ __launch_bounds__(256) void k_floor_final(FinalArgs A) {
     const int f = blockIdx.y;
