@@ -784,11 +784,15 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     }
     for (int k = tid; k <= M; k += FP_T) s_vv[k] = k == 0 ? sg * e[0] : (k == M ? sg * e[n - 1] : INF);
     __syncthreads();
-    /* valley -> its gap: gap g (between c_g and c_(g+1)) is s_vv[g + 1] */
+    /* valley -> its gap: gap g (between c_g and c_(g+1)) is s_vv[g + 1].
+     * Maxima and valleys alternate along the recording (between two maxima
+     * the samples fall to exactly one valley, plateaus included), so the
+     * wave's valley t has t of the wave's maxima before it, plus one when the
+     * wave's first extremum is a maximum */
+    const int vfirst = (cm > 0 && (cv == 0 || mp_g[w0 - 1] < vp_g[w0 - 1])) ? 1 : 0;
     for (int t = lane; t < cv; t += 64) {
         const int32_t pv = vp_g[w0 - 1 + t];
-        int lo = 0, hi = M;
-        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_mp[mid] < pv) lo = mid + 1; else hi = mid; }
+        const int lo = om + t + vfirst;
         const double val = sg * e[pv];
         if (lo == 0 || lo == M) s_vv[lo] = fmin(s_vv[lo], val);   /* edge gaps: at most one valley each */
         else s_vv[lo] = val;

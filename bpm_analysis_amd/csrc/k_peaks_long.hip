@@ -147,11 +147,12 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_fill(PeakArgs A, FplArgs L) {
         mh[off + t] = xv;
         st[off + t] = (!h || h[p] <= xv) ? open : ST_REMOVED;   /* height filter */
     }
+    /* maxima and valleys alternate (k_find_peaks_lds): the unit's valley t
+     * has t of its maxima before it, plus one when its first extremum is one */
+    const int vfirst = (cm > 0 && (cv == 0 || mp_u[0] < vp_u[0])) ? 1 : 0;
     for (int t = lane; t < cv; t += 64) {
         const int32_t pv = vp_u[t];
-        int lo = 0, hi = cm;                                 /* the unit's maxima before the valley */
-        while (lo < hi) { const int mid = (lo + hi) >> 1; if (mp_u[mid] < pv) lo = mid + 1; else hi = mid; }
-        const int g = off + lo;
+        const int g = off + t + vfirst;
         const double val = sg * e[pv];
         if (g == 0 || g == M) vv[g] = fmin(vv[g], val);      /* edge gaps: at most one valley each */
         else vv[g] = val;
@@ -462,21 +463,40 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_prom(PeakArgs A, FplArgs L) {
     const double INF = __builtin_inf();
     const double hj = mh[j];
     double lmin = INF, rmin = INF;
-    for (int k = j - 1;;) {
-        if (k < 0) { lmin = fmin(lmin, vv[0]); break; }
-        if ((k & 1023) == 1023 && bkh[k >> 10] <= hj) { lmin = fmin(lmin, bkl[k >> 10]); k -= 1024; continue; }
-        if ((k & 31) == 31 && b32h[k >> 5] <= hj) { lmin = fmin(lmin, b32l[k >> 5]); k -= 32; continue; }
-        lmin = fmin(lmin, vv[k + 1]);
-        if (mh[k] > hj) break;
-        --k;
-    }
-    for (int k = j + 1;;) {
-        if (k >= M) { rmin = fmin(rmin, vv[M]); break; }
-        if ((k & 1023) == 0 && k + 1023 < M && bkh[k >> 10] <= hj) { rmin = fmin(rmin, bkr[k >> 10]); k += 1024; continue; }
-        if ((k & 31) == 0 && k + 31 < M && b32h[k >> 5] <= hj) { rmin = fmin(rmin, b32r[k >> 5]); k += 32; continue; }
-        rmin = fmin(rmin, vv[k]);
-        if (mh[k] > hj) break;
-        ++k;
+    /* both walks step together and a step reads every candidate (the 1024-
+     * and 32-maximum block summaries, the gap valley, the maximum) before
+     * choosing: one memory round trip per step of both sides */
+    int kl = j - 1, kr = j + 1;
+    bool dl = false, dr = false;
+    while (!(dl && dr)) {
+        if (!dl) {
+            if (kl < 0) {
+                lmin = fmin(lmin, vv[0]);
+                dl = true;
+            } else {
+                const double h2 = bkh[kl >> 10], v2 = bkl[kl >> 10], h1 = b32h[kl >> 5], v1 = b32l[kl >> 5];
+                const double v0 = vv[kl + 1], m0 = mh[kl];
+                const bool c2 = (kl & 1023) == 1023 && h2 <= hj;
+                const bool c1 = !c2 && (kl & 31) == 31 && h1 <= hj;
+                lmin = fmin(lmin, c2 ? v2 : (c1 ? v1 : v0));
+                if (!(c2 || c1) && m0 > hj) dl = true;
+                else kl -= c2 ? 1024 : (c1 ? 32 : 1);
+            }
+        }
+        if (!dr) {
+            if (kr >= M) {
+                rmin = fmin(rmin, vv[M]);
+                dr = true;
+            } else {
+                const double h2 = bkh[kr >> 10], v2 = bkr[kr >> 10], h1 = b32h[kr >> 5], v1 = b32r[kr >> 5];
+                const double v0 = vv[kr], m0 = mh[kr];
+                const bool c2 = (kr & 1023) == 0 && kr + 1023 < M && h2 <= hj;
+                const bool c1 = !c2 && (kr & 31) == 0 && kr + 31 < M && h1 <= hj;
+                rmin = fmin(rmin, c2 ? v2 : (c1 ? v1 : v0));
+                if (!(c2 || c1) && m0 > hj) dr = true;
+                else kr += c2 ? 1024 : (c1 ? 32 : 1);
+            }
+        }
     }
     const double prom = hj - fmax(lmin, rmin);
     const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
