@@ -615,7 +615,9 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             InterpArgs a;
             a.env = O->env; a.doff = d_doff; a.troughs = tr; a.ntr = ntr; a.run = run; a.n_files = F;
             a.dense = dense; a.skip_n = use_wm ? WM_MMAX : -1; a.skip_gt = skip_gt;
-            LAUNCH(ctx, s, "k_interp", k_interp, g2, dim3(256), 0, s, a);
+            /* with no long recording only those with > WM_TRMAX troughs (rare): two workgroups each */
+            const dim3 gi = maxnd <= WM_MMAX && use_wm ? dim3(2, (unsigned)F) : g2;
+            LAUNCH(ctx, s, "k_interp", k_interp, gi, dim3(256), 0, s, a);
             return BPMX_OK;
         };
         auto rollq = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, double *outp,
@@ -639,7 +641,10 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 HIP_TRY(hipMemsetAsync(wm_fail, 0, (size_t)F * 4, s));
                 a.wm_chunk = (int32_t)wm_c;
             }
-            if ((rq_rc = interp(run, tr, ntr, wm_chunks ? WM_MMAX : INT64_MAX)) != BPMX_OK) return rq_rc;
+            /* the wavelet-matrix kernels interpolate every recording <= WM_MMAX
+             * themselves (from the troughs in LDS, or over global memory past
+             * WM_TRMAX troughs): dense only for the sorted-union kernels */
+            if (need_merge && (rq_rc = interp(run, tr, ntr, wm_chunks ? WM_MMAX : INT64_MAX)) != BPMX_OK) return rq_rc;
             if (use_wm) {
                 /* pruned structure first; recordings it cannot take (too many
                  * kept samples, > WM_TRMAX troughs) are flagged in wm_full for
@@ -724,10 +729,12 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
             const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);
-            a.vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 8, &rc);
+            a.vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 16, &rc);
             if (rc != BPMX_OK) return rc;
+            a.nund = a.vfl + 2 * F;
+            HIP_TRY(hipMemsetAsync(a.nund, 0, (size_t)F * 8, s));
             LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
-            const unsigned gp = (unsigned)std::max<int64_t>(1, (trmax + DP_CHUNK - 1) / DP_CHUNK);
+            const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8, (trmax + DP_CHUNK - 1) / DP_CHUNK));
             LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
             LAUNCH(ctx, s, "k_draft_points[wide]", k_draft_points<4>, dim3(F, gp), dim3(DB_T), 0, s, a);
         }

@@ -239,6 +239,8 @@ struct DraftBoundArgs {
     int64_t *stats;          /* optional (BPMX_OPT_STATS): += raw troughs, undecided troughs, chunks sent to the
                                 full draft by draft_point */
     int32_t *vfl;            /* [F][2] k_draft_bounds out: first / last valid draft output (k_draft_points) */
+    int32_t *nund;           /* [2F] zeroed before k_draft_bounds: undecided troughs per recording, then the
+                                ones k_draft_points<1> leaves to the [wide] launch */
 };
 /* k_draft_points: the undecided troughs of DP_CHUNK consecutive raw troughs per
  * workgroup, one wave per trough */

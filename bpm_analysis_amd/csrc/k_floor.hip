@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         uint8_t dcs;
         if (et <= A.mult * L) dcs = 1;
         else if (et > A.mult * U * (1.0 + 0x1p-50)) dcs = 0;
-        else dcs = 2;                                  /* k_draft_points */
+        else { dcs = 2; atomicAdd(&A.nund[f], 1); }     /* k_draft_points */
         A.dec[d0 + j] = dcs;
     }
     if (A.stats && tid == 0) atomicAdd((unsigned long long *)&A.stats[0], (unsigned long long)(jc1 - jc0));
@@ -1140,19 +1140,12 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
  * workgroup stages the troughs its windows reach.  A trough draft_point does
  * not take sends the recording to the full draft (exact). */
 template <int SPL>
-__global__ __launch_bounds__(DB_T, SPL == 1 ? BPMX_DP_WAVES : 1) void k_draft_points(DraftBoundArgs A) {
-    const int f = blockIdx.x;
-    if (f >= A.n_files || !A.run[f]) return;
-    const int m = A.nraw[f];
-    const int jc0 = (int)blockIdx.y * DP_CHUNK;
-    if (jc0 >= m) return;
+__device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int f, int m, int jc0, int32_t *s_tp,
+                                                   double *s_tv, int16_t *s_und, int *s_nund_p) {
+    int &s_nund = *s_nund_p;
     const int jc1 = min(m, jc0 + DP_CHUNK);
     const int tid = threadIdx.x;
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
-    __shared__ int32_t s_tp[DB_TRMAX];
-    __shared__ double s_tv[DB_TRMAX];
-    __shared__ int16_t s_und[DP_CHUNK];
-    __shared__ int s_nund;
     if (tid == 0) s_nund = 0;
     __syncthreads();
     for (int j = jc0 + tid; j < jc1; j += DB_T)
@@ -1206,7 +1199,10 @@ __global__ __launch_bounds__(DB_T, SPL == 1 ? BPMX_DP_WAVES : 1) void k_draft_po
          * case); wider ones stay undecided for the SPL 4 launch, so the
          * common kernel keeps the registers of one segment per lane */
         const int jl = seg_of(lo), jh = seg_of(hi - 1);
-        if (SPL == 1 && jh - jl + 1 > 64) continue;
+        if (SPL == 1 && jh - jl + 1 > 64) {                 /* for the [wide] launch */
+            if (lane_id() == 0) atomicAdd(&A.nund[A.n_files + f], 1);
+            continue;
+        }
         const uint32_t seed = 0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu;
         if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r)) {
             fail = true;
@@ -1217,6 +1213,24 @@ __global__ __launch_bounds__(DB_T, SPL == 1 ? BPMX_DP_WAVES : 1) void k_draft_po
     if (fail && lane_id() == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (A.stats && SPL == 1 && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
     if (A.stats && fail && lane_id() == 0) atomicAdd((unsigned long long *)&A.stats[2], 1ull);
+    __syncthreads();                                         /* s_und / s_nund reused by the next chunk */
+}
+
+/* a few workgroups per recording, each taking chunks y, y + gridDim.y, ...;
+ * recordings without undecided troughs (nund, from k_draft_bounds; the [wide]
+ * launch: none left for it) cost one load */
+template <int SPL>
+__global__ __launch_bounds__(DB_T, SPL == 1 ? BPMX_DP_WAVES : 1) void k_draft_points(DraftBoundArgs A) {
+    const int f = blockIdx.x;
+    if (f >= A.n_files || !A.run[f]) return;
+    if (A.nund[(SPL == 1 ? 0 : A.n_files) + f] == 0) return;
+    const int m = A.nraw[f];
+    __shared__ int32_t s_tp[DB_TRMAX];
+    __shared__ double s_tv[DB_TRMAX];
+    __shared__ int16_t s_und[DP_CHUNK];
+    __shared__ int s_nund;
+    for (int jc0 = (int)blockIdx.y * DP_CHUNK; jc0 < m; jc0 += (int)gridDim.y * DP_CHUNK)
+        draft_points_chunk<SPL>(A, f, m, jc0, s_tp, s_tv, s_und, &s_nund);
 }
 template __global__ void k_draft_points<1>(DraftBoundArgs);
 template __global__ void k_draft_points<DP_SPL_MAX>(DraftBoundArgs);

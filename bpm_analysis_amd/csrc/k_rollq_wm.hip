@@ -175,7 +175,11 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
      * table (a staged run that stops before the recording's last trough always
      * reaches past every position asked for) */
     auto dval = [&](int64_t x) -> double {
-        if (!fused) return dense[x];
+        if (!fused) {                                        /* > WM_TRMAX troughs: np.interp from global memory */
+            if (!A.env) return dense[x];
+            const int64_t *trg = A.troughs + d0;
+            return interp_at(x, trg, [&](int j) { return A.env[d0 + trg[j]]; }, ntr_all);
+        }
         if (ntr == 0 || x < s_tp[0]) return __builtin_nan("");
         int j = s_bj[(x - xb) >> 6];
         if (j < 0) j = 0;
