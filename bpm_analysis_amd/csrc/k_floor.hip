@@ -717,7 +717,7 @@ constexpr int DP_FIX = 4;         /* exact steps after a segment's inverse estim
 template <int DP_SPL>
 __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s_tv, int base, int m, int64_t n,
                                             int64_t lo, int64_t hi, int jl, int jh, double q, uint32_t seed,
-                                            double *res) {
+                                            double *res, double seedv = __builtin_nan(""), double *rho = nullptr) {
     const int lane = lane_id();
     if (jh - jl + 1 > 64 * DP_SPL) return false;
     int32_t sa[DP_SPL], sn[DP_SPL], st[DP_SPL], slo[DP_SPL], shi[DP_SPL], sub[DP_SPL];
@@ -764,6 +764,8 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
     int64_t below = 0, leq = -1;
     double va = 0.0;
     uint32_t rng = seed;
+    bool seed_down = false;
+    int64_t seed_nless = 0, seed_nleq = 0;
     for (int it = 0; it < 256; ++it) {
         int cnt = 0;
 #pragma unroll
@@ -804,6 +806,10 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             }
             const int t = (int)(k - below);
             va = __shfl(x, t);
+            if (rho) {                                       /* elements per unit value near the answer */
+                const double x0 = __shfl(x, 0), x1 = __shfl(x, tot - 1);
+                *rho = x1 > x0 ? (double)(tot - 1) / (x1 - x0) : __builtin_nan("");
+            }
             if (!interp) {
                 *res = va;
                 return true;
@@ -819,7 +825,16 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             return true;
         }
         double pv;
-        if (it < DP_IP_ROUNDS) {
+        if (it == 0 && __builtin_isfinite(seedv)) {
+            /* the neighbouring trough's draft value: its window overlaps this
+             * one but for a few segments, so the count there lands near k */
+            pv = seedv;
+        } else if (it == 1 && __builtin_isfinite(seedv) && rho && *rho > 0.0 && __builtin_isfinite(*rho)) {
+            /* then a step from it by the count still missing over the
+             * neighbour's density of values near its answer */
+            pv = seed_down ? seedv - ((double)(seed_nless - k) - 0.5) / *rho
+                           : seedv + ((double)(k - seed_nleq) + 0.5) / *rho;
+        } else if (it < DP_IP_ROUNDS) {
             /* a value pivot interpolated between the active extremes at the
              * target's rank: the values within a segment are evenly spaced, so
              * the active set shrinks by far more than a random pivot's half */
@@ -902,6 +917,7 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             ce += sub[r] - slo[r];
         }
         const int64_t nless = below + wave_sum_i(cl), nleq = below + wave_sum_i(ce);
+        if (it == 0) { seed_down = k < nless; seed_nless = nless; seed_nleq = nleq; }
         if (k < nless) {
 #pragma unroll
             for (int r = 0; r < DP_SPL; ++r) shi[r] = slb[r];
@@ -1148,8 +1164,13 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     if (tid == 0) s_nund = 0;
     __syncthreads();
-    for (int j = jc0 + tid; j < jc1; j += DB_T)
-        if (A.dec[d0 + j] == 2) s_und[atomicAdd(&s_nund, 1)] = (int16_t)(j - jc0);
+    if (tid < 64) {                                          /* in trough order (DP_CHUNK <= 64) */
+        const int j = jc0 + tid;
+        const bool und = j < jc1 && A.dec[d0 + j] == 2;
+        const uint64_t bm = __ballot(und);
+        if (und) s_und[__popcll(bm & ((1ull << tid) - 1ull))] = (int16_t)tid;
+        if (tid == 0) s_nund = __popcll(bm);
+    }
     __syncthreads();
     const int nu = s_nund;
     if (nu == 0) return;
@@ -1188,7 +1209,11 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
         return lo - 1;
     };
     bool fail = false;
-    for (int u = wave_id(); u < nu; u += DB_T / 64) {
+    /* each wave a run of consecutive undecided troughs, each seeded with the
+     * previous one's draft value */
+    const int per = (nu + DB_T / 64 - 1) / (DB_T / 64);
+    double prev = __builtin_nan(""), rho = __builtin_nan("");
+    for (int u = wave_id() * per; u < min(nu, (wave_id() + 1) * per); ++u) {
         const int j = jc0 + s_und[u];
         const int64_t t = s_tp[j - base];
         const int64_t qp = t < vf ? vf : (t > vl ? vl : t);
@@ -1204,10 +1229,11 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
             continue;
         }
         const uint32_t seed = 0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu;
-        if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r)) {
+        if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r, prev, &rho)) {
             fail = true;
             continue;
         }
+        prev = r;
         if (lane_id() == 0) A.dec[d0 + j] = (r == r && s_tv[j - base] <= A.mult * r) ? 1 : 0;
     }
     if (fail && lane_id() == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
