@@ -415,8 +415,11 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
 #undef ENV_REF
 #undef ENV_REF_K
             if (chain)
-                LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean, dim3((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64)),
-                       dim3(256), 0, s, a);
+            {
+                const dim3 gm((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64));
+                if (a.y) LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean<true>, gm, dim3(256), 0, s, a);
+                else LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean<false>, gm, dim3(256), 0, s, a);
+            }
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
             if (r != BPMX_OK) return r;

@@ -33,6 +33,7 @@ struct EnvRefArgs {
     unsigned long long *stamps;
 #endif
 };
+template <bool WANT_Y>
 __global__ void k_ref_env_mean(EnvRefArgs A);
 template <bool ZB>
 __global__ void k_ref_fwd(EnvRefArgs A);

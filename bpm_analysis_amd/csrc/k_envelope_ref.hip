@@ -587,9 +587,11 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
  * of equal added values ending there is counted back (it only matters up to
  * nobs).  A tile of 64 steps x 64 recordings, transposed through LDS so the
  * stores are contiguous; the y output (when requested) rides along. */
+template <bool WANT_Y>
 __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
+    /* without the y output the staging is half the LDS: four workgroups per CU */
     __shared__ double st_env[STG][65];
-    __shared__ double st_y[STG][65];
+    __shared__ double st_y[WANT_Y ? STG : 1][65];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int f = blockIdx.y * 64 + lane;
     const bool have = f < A.n_files;
@@ -615,7 +617,7 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
         sm[r] = ok ? sums[(ic >> 1) * S * 2 + (ic & 1)] : 0.0;
         ya[r] = ok ? y[a * S] : 0.0;
         yb[r] = ok && a > 0 ? y[(a - 1) * S] : 0.0;
-        yi[r] = ok ? y[ic * S] : 0.0;
+        yi[r] = WANT_Y && ok ? y[ic * S] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -638,7 +640,7 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
             ev = nobs >= 1 ? res : __builtin_nan("");
         }
         st_env[wv * R + r][lane] = ev;
-        st_y[wv * R + r][lane] = yi[r];
+        if (WANT_Y) st_y[wv * R + r][lane] = yi[r];
     }
     __syncthreads();
     for (int fl = wv; fl < 64; fl += 4) {
@@ -647,11 +649,13 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
         const int64_t i = i00 + lane;
         if (i < fnd) {
             A.env[fd0 + i] = st_env[lane][fl];
-            if (A.y) A.y[fd0 + i] = st_y[lane][fl];
+            if (WANT_Y) A.y[fd0 + i] = st_y[lane][fl];
         }
     }
 }
 
+template __global__ void k_ref_env_mean<true>(EnvRefArgs);
+template __global__ void k_ref_env_mean<false>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_U8, false>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_I16, false>(EnvRefArgs);
 template __global__ void k_ref_pick<BPMX_DT_I32, false>(EnvRefArgs);
