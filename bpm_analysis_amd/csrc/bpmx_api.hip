@@ -366,9 +366,22 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             const bool split = nfc >= 2 && !(P->options & BPMX_OPT_REF_NOSPLIT) && ctx->side_ready() &&
                                ctx->ref_events((size_t)nfc);
             a.pick_r0 = 0; a.fwd_rb = 0; a.fwd_re = 0; a.fwd_z = nullptr;
+            a.kahan_z = nullptr; a.kahan_ib = 0; a.kahan_ie = 0; a.mean_r0 = 0;
             if (split) {
                 a.fwd_z = (double *)ctx->buf("ref_fwd_z", (size_t)F * 4 * 8, &rc);
                 if (rc != BPMX_OK) return rc;
+            }
+            /* chain mode: the Kahan pass in row chunks ending at 1/2, 3/4, 7/8
+             * and all of the rows, each finished chunk's means formed by
+             * k_ref_env_mean on the side stream while the next chunk runs */
+            int64_t kend[4] = {0, 0, 0, 0};
+            int nkc = 0;
+            if (chain && split && maxnd >= 4096 && ctx->ref_events((size_t)nfc + 8)) {
+                for (int k = 1; k <= 3; ++k) kend[nkc++] = (maxnd - (maxnd >> k)) & ~(int64_t)63;
+                kend[nkc++] = maxnd;
+                a.kahan_z = (double *)ctx->buf("ref_kahan_z", (size_t)F * 6 * 8, &rc);
+                if (rc != BPMX_OK) return rc;
+                a.kahan_ie = kend[0];
             }
             auto env_ref = [&](void (*pick)(EnvRefArgs), void (*body)(EnvRefArgs), void (*fwd)(EnvRefArgs)) -> int {
                 if (!split) {
@@ -414,11 +427,32 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             if (rc != BPMX_OK) return rc;
 #undef ENV_REF
 #undef ENV_REF_K
-            if (chain)
-            {
+            if (chain && !a.kahan_z) {
                 const dim3 gm((unsigned)((maxnd + 63) / 64), (unsigned)((F + 63) / 64));
                 if (a.y) LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean<true>, gm, dim3(256), 0, s, a);
                 else LAUNCH(ctx, s, "k_ref_env_mean", k_ref_env_mean<false>, gm, dim3(256), 0, s, a);
+            } else if (chain) {
+                hipStream_t s2 = ctx->side[0];
+                EnvRefArgs c = a;
+                for (int k = 0; k < nkc; ++k) {
+                    if (k > 0) {                             /* steps [kend[k-1], kend[k]) */
+                        c.kahan_ib = kend[k - 1];
+                        c.kahan_ie = kend[k];
+                        LAUNCH(ctx, s, "k_ref_kahan", k_ref_kahan, g, b, 0, s, c);
+                    }
+                    hipEvent_t ek = ctx->ref_ev[nfc + k];
+                    HIP_TRY(hipEventRecord(ek, s));
+                    HIP_TRY(hipStreamWaitEvent(s2, ek, 0));
+                    const int64_t r0 = k > 0 ? kend[k - 1] : 0;
+                    EnvRefArgs mk = a;
+                    mk.mean_r0 = r0;
+                    const dim3 gm((unsigned)((kend[k] - r0 + 63) / 64), (unsigned)((F + 63) / 64));
+                    if (a.y) LAUNCH(ctx, s2, "k_ref_env_mean", k_ref_env_mean<true>, gm, dim3(256), 0, s2, mk);
+                    else LAUNCH(ctx, s2, "k_ref_env_mean", k_ref_env_mean<false>, gm, dim3(256), 0, s2, mk);
+                }
+                hipEvent_t ej = ctx->ref_ev[nfc + 4];
+                HIP_TRY(hipEventRecord(ej, s2));
+                HIP_TRY(hipStreamWaitEvent(s, ej, 0));
             }
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);

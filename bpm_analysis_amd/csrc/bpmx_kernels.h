@@ -29,6 +29,11 @@ struct EnvRefArgs {
      * [F][4] between chunks; fwd_z null: k_envelope_ref_t runs the forward pass */
     int64_t fwd_rb, fwd_re;
     double *fwd_z;
+    /* chunked Kahan pass (chain mode): k_envelope_ref_t runs steps [0,
+     * kahan_ie), k_ref_kahan [kahan_ib, kahan_ie), the RollMean state [F][6]
+     * in kahan_z (null: one pass); k_ref_env_mean forms rows from mean_r0 */
+    double *kahan_z;
+    int64_t kahan_ib, kahan_ie, mean_r0;
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
@@ -37,6 +42,7 @@ template <bool WANT_Y>
 __global__ void k_ref_env_mean(EnvRefArgs A);
 template <bool ZB>
 __global__ void k_ref_fwd(EnvRefArgs A);
+__global__ void k_ref_kahan(EnvRefArgs A);
 constexpr int64_t REF_FWD_ROWS = 1024;   /* first forward chunk's rows, doubling per chunk (multiples of the prefetch block) */
 
 struct QuantArgs {

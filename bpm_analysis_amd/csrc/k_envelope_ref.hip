@@ -98,6 +98,16 @@ struct Df2t {
 struct RollMean {
     double sum = 0, cadd = 0, crem = 0, prev = 0;
     int32_t nobs = 0, neg = 0, same = 0;   /* <= recording length (< 2^31, host-checked) */
+    /* exact copies across the launches of a chunked pass: 6 doubles */
+    __device__ __forceinline__ void save(double *z) const {
+        z[0] = sum; z[1] = cadd; z[2] = crem; z[3] = prev;
+        z[4] = __longlong_as_double(((long long)nobs << 32) | (unsigned)neg); z[5] = __longlong_as_double(same);
+    }
+    __device__ __forceinline__ void load(const double *z) {
+        sum = z[0]; cadd = z[1]; crem = z[2]; prev = z[3];
+        const long long a = __double_as_longlong(z[4]);
+        nobs = (int32_t)(a >> 32); neg = (int32_t)(unsigned)(a & 0xFFFFFFFFll); same = (int32_t)__double_as_longlong(z[5]);
+    }
     __device__ __forceinline__ void add(double v) {
         if (v == v) {
             nobs++;
@@ -227,7 +237,8 @@ __global__ __launch_bounds__(256) void k_ref_pick(EnvRefArgs A) {
 template <int W>
 __device__ __forceinline__ void kahan_chain(RollMean &R, const double *__restrict__ y, double *__restrict__ ps,
                                             int64_t S, int64_t off, int64_t w, int64_t nd, int64_t ndmax,
-                                            int64_t ndmin, bool run, int64_t last) {
+                                            int64_t ndmin, bool run, int64_t last, int64_t ib = 0,
+                                            int64_t ie = INT64_MAX) {
     static_assert(W <= PF, "the remove value must lie within the previous block");
     auto ldy = [&](int64_t i) -> double {
         i = i < 0 ? 0 : (i > last ? last : i);
@@ -235,16 +246,19 @@ __device__ __forceinline__ void kahan_chain(RollMean &R, const double *__restric
     };
     typedef double dv2 __attribute__((ext_vector_type(2)));
     auto put = [&](int64_t i, double v) { ps[(i >> 1) * S * 2 + (i & 1)] = v; };
-    const double *pa = y + off * S, *pr = y + (off - w) * S;   /* rows i0 + off, i0 + off - w */
+    /* steps [ib, ie) (ib a multiple of PF): the pass in row chunks, R carried between them */
+    ps += (ib >> 1) * S * 2;
+    const double *pa = y + (ib + off) * S, *pr = y + (ib + off - w) * S;   /* rows i0 + off, i0 + off - w */
     const int64_t SP = (int64_t)PF * S;
     double ca[PF], na[PF], cp[PF], cr[W == 0 ? PF : 1], nr[W == 0 ? PF : 1];
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-        ca[u] = ldy(u + off);
-        cp[u] = ldy(u + off - PF);
-        if (W == 0) cr[u] = ldy(u + off - w);
+        ca[u] = ldy(ib + u + off);
+        cp[u] = ldy(ib + u + off - PF);
+        if (W == 0) cr[u] = ldy(ib + u + off - w);
     }
-    for (int64_t i0 = 0; i0 < ndmax; i0 += PF, ps += SP, pa += SP, pr += SP) {
+    const int64_t iend = ie < ndmax ? ie : ndmax;
+    for (int64_t i0 = ib; i0 < iend; i0 += PF, ps += SP, pa += SP, pr += SP) {
         if (i0 + PF + off - w >= 0 && i0 + 2 * PF + off <= ndmin) {
 #pragma unroll
             for (int u = 0; u < PF; ++u) {
@@ -372,6 +386,39 @@ __global__ __launch_bounds__(64) void k_ref_fwd(EnvRefArgs A) {
 }
 template __global__ void k_ref_fwd<false>(EnvRefArgs);
 template __global__ void k_ref_fwd<true>(EnvRefArgs);
+
+/* The rolling mean's Kahan recursion over steps [kahan_ib, kahan_ie) of the
+ * chain mode, R carried in kahan_z: the pass runs in row chunks so that
+ * k_ref_env_mean forms the finished chunks' means on a side stream meanwhile.
+ * Waves whose recordings left chain mode (a NaN in |y|) did their whole pass
+ * in k_envelope_ref_t. */
+__global__ __launch_bounds__(64) void k_ref_kahan(EnvRefArgs A) {
+    const int lane = threadIdx.x;
+    const int f = blockIdx.x * 64 + lane;
+    const bool have = f < A.n_files;
+    int64_t nd = have ? A.doff[f + 1] - A.doff[f] : 0;
+    const bool run = have && nd > 15 && A.active[f];
+    if (!run) nd = 0;
+    if (!__ballot(have && A.chain[f])) return;              /* not chain mode, or nothing to run */
+    int64_t ndmax = nd;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmax, o); ndmax = t > ndmax ? t : ndmax; }
+    int64_t ndmin = run ? nd : INT64_MAX;
+    for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(ndmin, o); ndmin = t < ndmin ? t : ndmin; }
+    const int64_t S = A.n_files, w = A.env_window, off = (w - 1) / 2;
+    const int64_t last = nd > 0 ? nd - 1 : 0;
+    const double *__restrict__ y = A.scratch + (have ? f : 0) + 15 * S;
+    double *__restrict__ ps = A.sums + (have ? (int64_t)f * 2 : 0);
+    RollMean R;
+    if (have) R.load(A.kahan_z + (int64_t)f * 6);
+    const int64_t ib = A.kahan_ib, ie = A.kahan_ie;
+    switch (w) {
+    case 30: kahan_chain<30>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, ib, ie); break;
+    case 31: kahan_chain<31>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, ib, ie); break;
+    case 32: kahan_chain<32>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, ib, ie); break;
+    default: kahan_chain<0>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, ib, ie); break;
+    }
+    if (have) R.save(A.kahan_z + (int64_t)f * 6);
+}
 
 template <int DT, bool MULTI, bool ZB>
 __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
@@ -512,12 +559,14 @@ __global__ __launch_bounds__(64) void k_envelope_ref_t(EnvRefArgs A) {
         if (chain) {
             /* only the Kahan recursion; k_ref_env_mean forms the means */
             double *__restrict__ ps = A.sums + (have ? (int64_t)f * 2 : 0);   /* pair rows [i / 2][file][2] */
+            const int64_t ie = A.kahan_z ? A.kahan_ie : INT64_MAX;   /* chunked: the first chunk here */
             switch (w) {
-            case 30: kahan_chain<30>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
-            case 31: kahan_chain<31>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
-            case 32: kahan_chain<32>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
-            default: kahan_chain<0>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last); break;
+            case 30: kahan_chain<30>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, 0, ie); break;
+            case 31: kahan_chain<31>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, 0, ie); break;
+            case 32: kahan_chain<32>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, 0, ie); break;
+            default: kahan_chain<0>(R, y, ps, S, off, w, nd, ndmax, ndmin, run, last, 0, ie); break;
             }
+            if (A.kahan_z && have) R.save(A.kahan_z + (int64_t)f * 6);
             STAMP(2);
             STAMP_FLUSH(A.stamps);
             return;
@@ -599,7 +648,7 @@ __global__ __launch_bounds__(256) void k_ref_env_mean(EnvRefArgs A) {
     const int64_t nd = have ? A.doff[f + 1] - A.doff[f] : 0;
     const int64_t d0 = have ? A.doff[f] : 0;
     const int64_t S = A.n_files, w = A.env_window, off = (w - 1) / 2;
-    const int64_t i00 = (int64_t)blockIdx.x * STG;
+    const int64_t i00 = A.mean_r0 + (int64_t)blockIdx.x * STG;
     if (!__syncthreads_or(mine && i00 < nd)) return;
     const double *__restrict__ y = A.scratch + 15 * S + (have ? f : 0);
     const double *__restrict__ sums = A.sums + (have ? (int64_t)f * 2 : 0);     /* pair rows [i / 2][file][2] */
