@@ -1013,3 +1013,31 @@ def test_longfft_hilbert_matches_bluestein_and_oracle(det):
     o = O.detect(O.synth(321 + 2, lens[2], fs, 1), fs, params, mode="native")     # odd Nd = 95,993 = 59 x 1627
     assert len(a[2]["env"]) == 95_993
     _check_file(a[2], o, exact_env=False)
+
+
+def test_reference_split_passes_bit_identical(det):
+    """Reference mode runs the forward pass in row chunks beside the gather of
+    the next chunks (k_ref_fwd), and the Kahan pass in row chunks beside the
+    finished chunks' means (k_ref_kahan, k_ref_env_mean on a side stream).
+    Those splits equal the single-kernel passes (BPMX_OPT_REF_NOSPLIT) and the
+    fully serial rolling mean (BPMX_OPT_REF_SERIAL_MEAN) bit for bit, on a
+    ragged f32 batch over two waves of recordings, one of them holding a NaN
+    (its wave leaves chain mode and keeps the in-pass means), y included; and
+    the clean recordings equal the oracle."""
+    from bpm_analysis_amd import _native as N
+    fs = 44100
+    rng = np.random.default_rng(17)
+    lens = [int(fs * s) for s in rng.uniform(14.0, 24.0, 70)]
+    recs = [O.synth(400 + f, n, fs, 1).astype(np.float32) for f, n in enumerate(lens)]
+    recs[3][len(recs[3]) // 2] = np.nan                     # wave 0 leaves chain mode
+    params = dict(G.BASE_PARAMS)
+    a = det.run_host(recs, fs, params, mode="reference", want_y=True)
+    b = det.run_host(recs, fs, params, mode="reference", want_y=True, options=N.OPT_REF_NOSPLIT)
+    c = det.run_host(recs, fs, params, mode="reference", want_y=True, options=N.OPT_REF_SERIAL_MEAN)
+    for x, y, z in zip(a, b, c):
+        for k in ("env", "y", "floor", "troughs", "peaks"):
+            assert _same(x[k], y[k]) and _same(x[k], z[k]), k
+        assert x["flags"] == y["flags"] == z["flags"]
+    for f in (0, 1, 40, 69):
+        o = O.detect(recs[f], fs, params, mode="reference")
+        assert _same(a[f]["env"], o["env"]) and _same(a[f]["peaks"], o["peaks"]), f
