@@ -44,13 +44,15 @@ namespace {
 /* per-run output init from the cached device geometry (no pageable H2D copy
  * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
 __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *active, int32_t *flags, int32_t *ntr,
-                                                  int32_t *npk, int32_t *runs) {
+                                                  int32_t *npk, int32_t *runs, int32_t *z1, int32_t *z2) {
     const int f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n_files) return;
     flags[f] = active[f] ? 0 : BPMX_F_TOO_SHORT;
     if (ntr) ntr[f] = 0;
     if (npk) npk[f] = 0;
     for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
+    if (z1) z1[f] = 0;                                       /* draft exact masks (one int per recording) */
+    if (z2) { z2[2 * f] = 0; z2[2 * f + 1] = 0; }            /* draft undecided counters (two ints) */
 }
 
 /* recordings with >= 5 raw troughs reach the rolling quantile: with a noise
@@ -325,8 +327,18 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     const int32_t *d_active = di;
     int32_t *d_run1 = di + F, *d_run2 = di + 2 * F, *d_an1 = di + 3 * F, *d_an2 = di + 4 * F, *d_nraw = di + 5 * F;
 
+    /* the draft bracket's per-recording masks and counters (FLOOR below) are
+     * zeroed here, with the outputs, instead of by two memset launches */
+    const bool bounds = do_floor && !(P->options & BPMX_OPT_DRAFT_FULL);
+    int32_t *draft_masks = nullptr, *draft_vfl = nullptr;
+    if (bounds) {
+        draft_masks = (int32_t *)ctx->buf("draft_masks", (size_t)F * 8, &rc);
+        draft_vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 16, &rc);
+        if (rc != BPMX_OK) return rc;
+    }
     LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, F, d_active, (int32_t *)O->flags,
-           do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1);
+           do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1,
+           draft_masks, bounds ? draft_vfl + 2 * F : nullptr);
 
     /* ---- ENVELOPE ---- */
     if (do_env) {
@@ -746,16 +758,13 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
          * bracket skip the full rolling quantile; the others (and, after
          * sanitize, bounded ones left with <= 2 troughs, whose floor IS the
          * draft) get it exactly.  BPMX_OPT_DRAFT_FULL forces it for all. */
-        const bool bounds = !(P->options & BPMX_OPT_DRAFT_FULL);
         uint8_t *tdec = nullptr;
         int32_t *d_exact = d_run1, *d_runfb = nullptr;
         if (bounds) {
             tdec = (uint8_t *)ctx->buf("trough_dec", (size_t)sumnd, &rc);
-            int32_t *fl2 = (int32_t *)ctx->buf("draft_masks", (size_t)F * 8, &rc);
             if (rc != BPMX_OK) return rc;
-            d_exact = fl2;
-            d_runfb = fl2 + F;
-            HIP_TRY(hipMemsetAsync(d_exact, 0, (size_t)F * 4, s));
+            d_exact = draft_masks;                             /* zeroed by k_init_out */
+            d_runfb = draft_masks + F;
             DraftBoundArgs a;
             a.env = O->env; a.doff = d_doff; a.raw = rawt; a.nraw = d_nraw; a.run = d_run1; a.n_files = F;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
@@ -766,10 +775,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             /* find_peaks' distance spaces the troughs, so a recording has at most Nd / distance + 1 */
             const int64_t trmax = maxnd / std::max<int64_t>(1, P->distance) + 1;
             const unsigned gy = (unsigned)std::max<int64_t>(1, (trmax + DB_T - 1) / DB_T);
-            a.vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 16, &rc);
-            if (rc != BPMX_OK) return rc;
-            a.nund = a.vfl + 2 * F;
-            HIP_TRY(hipMemsetAsync(a.nund, 0, (size_t)F * 8, s));
+            a.vfl = draft_vfl;
+            a.nund = draft_vfl + 2 * F;                        /* zeroed by k_init_out */
             LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
             const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8, (trmax + DP_CHUNK - 1) / DP_CHUNK));
             LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
