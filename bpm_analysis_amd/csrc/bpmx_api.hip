@@ -44,13 +44,15 @@ namespace {
 /* per-run output init from the cached device geometry (no pageable H2D copy
  * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
 __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *active, int32_t *flags, int32_t *ntr,
-                                                  int32_t *npk, int32_t *runs, int32_t *z1, int32_t *z2) {
+                                                  int32_t *npk, int32_t *runs, int32_t *nraw, int32_t *z1,
+                                                  int32_t *z2) {
     const int f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n_files) return;
     flags[f] = active[f] ? 0 : BPMX_F_TOO_SHORT;
     if (ntr) ntr[f] = 0;
     if (npk) npk[f] = 0;
     for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
+    if (nraw) nraw[f] = 0;                                   /* the caller's raw-trough counts */
     if (z1) z1[f] = 0;                                       /* draft exact masks (one int per recording) */
     if (z2) { z2[2 * f] = 0; z2[2 * f + 1] = 0; }            /* draft undecided counters (two ints) */
 }
@@ -325,7 +327,9 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     }
     const int64_t *d_foff = dgeo, *d_doff = dgeo + F + 1, *d_boff = dgeo + 2 * (F + 1);
     const int32_t *d_active = di;
-    int32_t *d_run1 = di + F, *d_run2 = di + 2 * F, *d_an1 = di + 3 * F, *d_an2 = di + 4 * F, *d_nraw = di + 5 * F;
+    int32_t *d_run1 = di + F, *d_run2 = di + 2 * F, *d_an1 = di + 3 * F, *d_an2 = di + 4 * F;
+    /* raw-trough counts go straight into the caller's array when it asks for them */
+    int32_t *d_nraw = (do_floor && O->n_raw_troughs) ? (int32_t *)O->n_raw_troughs : di + 5 * F;
 
     /* the draft bracket's per-recording masks and counters (FLOOR below) are
      * zeroed here, with the outputs, instead of by two memset launches */
@@ -338,7 +342,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     }
     LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, F, d_active, (int32_t *)O->flags,
            do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1,
-           draft_masks, bounds ? draft_vfl + 2 * F : nullptr);
+           d_nraw != di + 5 * F ? d_nraw : nullptr, draft_masks, bounds ? draft_vfl + 2 * F : nullptr);
 
     /* ---- ENVELOPE ---- */
     if (do_env) {
@@ -751,8 +755,6 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             LAUNCH(ctx, s, "k_rollq_fill", k_rollq_fill, dim3(4, (unsigned)F), dim3(256), 0, s, fill);
             return BPMX_OK;
         };
-        if (O->n_raw_troughs)
-            HIP_TRY(hipMemcpyAsync(O->n_raw_troughs, d_nraw, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
         /* Draft floor: sanitize reads it at the raw troughs only, so the
          * recordings whose every keep decision follows from k_draft_bounds'
          * bracket skip the full rolling quantile; the others (and, after

@@ -62,8 +62,13 @@ def test_ragged_batch_matches_single(det):
     recs = [g["pcm"] for g in gs[:2]] + [short] + [g["pcm"] for g in gs[2:]]
     res = det.run_host(recs, 44100, G.BASE_PARAMS, mode="reference")
     assert res[2]["flags"] & 8
+    assert res[2]["n_raw_troughs"] == 0
+    d = O.derive(44100, G.BASE_PARAMS)
     for r, g in zip(res[:2] + res[3:], gs):
         _check_file(r, g)
+        # the "Kept X of Y initial troughs" count (bpm_analysis.py:1067-1069, :1099)
+        prom = O.quantile(g["env"], G.BASE_PARAMS["trough_prominence_quantile"])
+        assert r["n_raw_troughs"] == len(O.find_peaks(g["env"], distance=d.distance, prominence=prom, negate=True))
 
 
 @pytest.mark.parametrize("name", G.names(kind="env"))
