@@ -35,7 +35,7 @@ METRIC = "audio-samples/sec (filter+envelope+peaks), 1024x60s@44.1kHz batch, 1 &
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # flags both sides report: static / draft / NaN floor (BPMX_F_TOO_SHORT and
 # BPMX_F_BAD_WINDOW are library-side input checks, compared by the tests)
-FLOOR_FLAGS = 1 | 2 | 4
+FLOOR_FLAGS = 1 | 2 | 4 | 32 | 64      # fallbacks and the decisive-tie reports (bpmx.h)
 
 
 def parse(argv=None):

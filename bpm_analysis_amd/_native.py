@@ -20,6 +20,7 @@ DT_U8, DT_I16, DT_I32, DT_F32, DT_F64 = 0, 1, 2, 3, 4
 MODE_REFERENCE, MODE_NATIVE = 0, 1
 STAGE_ENVELOPE, STAGE_FLOOR, STAGE_PEAKS, STAGE_ALL = 1, 2, 4, 7
 F_STATIC_FLOOR, F_DRAFT_FLOOR, F_NAN_FLOOR, F_TOO_SHORT, F_BAD_WINDOW = 1, 2, 4, 8, 16
+F_TROUGH_TIE, F_PEAK_TIE = 32, 64      # decisive height tie in find_peaks' distance filter (bpmx.h)
 OPT_ROLLQ_MERGE = 1
 OPT_NATIVE_F64 = 2
 OPT_HILBERT_ROCFFT = 4

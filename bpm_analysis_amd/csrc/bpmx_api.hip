@@ -519,7 +519,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     const dim3 g_dch((unsigned)((maxnd / 2 + 1 + FPC_S - 1) / FPC_S), (unsigned)F);
 #define FIND_PEAKS(A, TAG)                                                                                  \
     do {                                                                                                   \
-        (A).vcand = vcand; (A).fallback = fp_fb; (A).only = nullptr;                                      \
+        (A).vcand = vcand; (A).fallback = fp_fb; (A).only = nullptr; (A).flags = (int32_t *)O->flags;     \
         (A).lds_nmax = fp_long ? FPL_NMIN : INT64_MAX;                                                     \
         if (!fp_global) {                                                                                  \
             LAUNCH(ctx, s, "k_find_peaks[" TAG "]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, (A));    \
@@ -612,7 +612,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.env = O->env; a.height = nullptr; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
-            a.run_out = d_run1; a.run_min = 5;
+            a.run_out = d_run1; a.run_min = 5; a.tie_bit = BPMX_F_TROUGH_TIE;
             FIND_PEAKS(a, "troughs");
         }
         if (bad_window)
@@ -808,7 +808,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.env = O->env; a.height = O->floor; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
-        a.run_out = nullptr; a.run_min = 0;
+        a.run_out = nullptr; a.run_min = 0; a.tie_bit = BPMX_F_PEAK_TIE;
         FIND_PEAKS(a, "peaks");
     }
 #undef FIND_PEAKS

@@ -119,13 +119,21 @@ struct PeakArgs {
     int32_t *fallback;     /* k_find_peaks_lds: [F] out, 1 = too many maxima for LDS (k_find_peaks takes it) */
     const int32_t *only;   /* k_find_peaks / k_fpl_*: [F] or null, process only recordings with only[f] != 0 */
     int64_t lds_nmax;      /* k_find_peaks_lds: hand recordings longer than this over (fallback = 1) */
+    int32_t *flags;        /* [F] per-file flags: tie_bit is OR'd in when the distance filter met a decisive tie */
+    int32_t tie_bit;       /* BPMX_F_TROUGH_TIE or BPMX_F_PEAK_TIE */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif
 };
 
-/* find_peaks candidate states (k_find_peaks, k_find_peaks_lds, k_fpl_*) */
-enum { ST_UNDECIDED = 0, ST_KEPT = 1, ST_REMOVED = 2, ST_FINAL = 3 };
+/* find_peaks candidate states (k_find_peaks, k_find_peaks_lds, k_fpl_*).
+ * Every state a candidate reaches after the distance filter kept it is odd
+ * (KEPT, then FINAL or PREMOVED by the prominence threshold), so the decisive-
+ * tie check (st_kept_by_distance) reads the distance outcome while other
+ * threads are already overwriting it with the prominence outcome.  REMOVED is
+ * reserved for the distance filter's removals; the height filter has its own. */
+enum { ST_UNDECIDED = 0, ST_KEPT = 1, ST_REMOVED = 2, ST_FINAL = 3, ST_HEIGHT = 4, ST_PREMOVED = 5 };
+__device__ __forceinline__ bool st_kept_by_distance(uint8_t s) { return (s & 1u) != 0; }
 
 __device__ __forceinline__ uint8_t ld_state(const uint8_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -446,7 +446,7 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     const double sg = A.sign;
     const int tid = threadIdx.x;
     __shared__ int sh[FP_T / 64 + 1];
-    __shared__ int s_flag;
+    __shared__ int s_flag, s_tie;
     __shared__ double s_bmx[FP_NBMAX], s_bmn[FP_NBMAX];
     __shared__ double s_cv[FP_MC];
     __shared__ int32_t s_cp[FP_MC];
@@ -554,6 +554,7 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     /* (3) distance: rounds of local decisions */
     const int64_t dist = A.distance;
     for (int j = tid; j < m; j += FP_T) st_state(&st[j], dist > 1 ? ST_UNDECIDED : ST_KEPT);
+    if (tid == 0) s_tie = 0;
     __syncthreads();
     if (dist > 1) {
         /* every round decides at least the highest-priority undecided candidate,
@@ -596,6 +597,21 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     }
 
     STAMP(2);
+    /* decisive tie (include/bpmx.h BPMX_F_*_TIE): a removed candidate with no
+     * strictly higher kept candidate within dist was removed by an equal one */
+    if (dist > 1) {
+        for (int j = tid; j < m; j += FP_T) {
+            if (ld_state(&st[j]) != ST_REMOVED) continue;
+            const int64_t pj = cp[j];
+            const double vj = cval(j);
+            bool dom = false;
+            for (int k = j - 1; !dom && k >= 0 && pj - cp[k] < dist; --k)
+                dom = cval(k) > vj && st_kept_by_distance(ld_state(&st[k]));
+            for (int k = j + 1; !dom && k < m && cp[k] - pj < dist; ++k)
+                dom = cval(k) > vj && st_kept_by_distance(ld_state(&st[k]));
+            if (!dom) s_tie = 1;
+        }
+    }
     /* (4) prominences of the kept candidates, one wave each */
     const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
     /* the kept candidates are taken NP at a time per wave so that their global
@@ -625,7 +641,7 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
             if (lane_id() == 0) {
 #pragma unroll
                 for (int c = 0; c < NP; ++c)
-                    if (jj[c] >= 0) st_state(&st[jj[c]], thr <= pr[c] ? ST_FINAL : ST_REMOVED);
+                    if (jj[c] >= 0) st_state(&st[jj[c]], thr <= pr[c] ? ST_FINAL : ST_PREMOVED);
             }
         }
     }
@@ -657,6 +673,7 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     if (tid == 0) {
         A.nout[f] = w;
         if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
+        if (s_tie && A.flags) A.flags[f] |= A.tie_bit;
     }
     STAMP(4);
     STAMP_FLUSH(A.stamps);
@@ -713,6 +730,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     __shared__ double s_bh[FL_B1 + FL_B2 + FL_B3], s_bvl[FL_B1 + FL_B2 + FL_B3], s_bvr[FL_B1 + FL_B2 + FL_B3];
     __shared__ int s_gc[2][FP_G][NW];
     __shared__ int sh[NW + 1];
+    __shared__ int s_tie;
     STAMP_DECL
 
     /* (1) local maxima (plateau midpoints) and valley starts, in order: wave w
@@ -780,8 +798,9 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         const int k = om + t;
         s_mp[k] = p;
         s_mh[k] = xv;
-        s_st[k] = (!h || h[p] <= xv) ? (dist > 1 ? ST_UNDECIDED : ST_KEPT) : ST_REMOVED;   /* height filter */
+        s_st[k] = (!h || h[p] <= xv) ? (dist > 1 ? ST_UNDECIDED : ST_KEPT) : ST_HEIGHT;   /* height filter */
     }
+    if (tid == 0) s_tie = 0;
     for (int k = tid; k <= M; k += FP_T) s_vv[k] = k == 0 ? sg * e[0] : (k == M ? sg * e[n - 1] : INF);
     __syncthreads();
     /* valley -> its gap: gap g (between c_g and c_(g+1)) is s_vv[g + 1].
@@ -941,7 +960,23 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
         const double *bh2 = s_bh + FL_B1, *bh3 = s_bh + FL_B1 + FL_B2;
         for (int j = tid; j < M; j += FP_T) {
-            if (s_st[j] != ST_KEPT) continue;
+            const uint8_t sj = ld_state(&s_st[j]);
+            if (sj == ST_REMOVED) {
+                /* removed by the distance filter: a decisive tie (include/bpmx.h
+                 * BPMX_F_*_TIE) unless a strictly higher candidate the filter
+                 * kept lies within dist (its state may already carry the
+                 * prominence outcome: every kept state is odd) */
+                const int64_t pj = s_mp[j];
+                const double vj = s_mh[j];
+                bool dom = false;
+                for (int k = j - 1; !dom && k >= 0 && pj - s_mp[k] < dist; --k)
+                    dom = s_mh[k] > vj && st_kept_by_distance(ld_state(&s_st[k]));
+                for (int k = j + 1; !dom && k < M && s_mp[k] - pj < dist; ++k)
+                    dom = s_mh[k] > vj && st_kept_by_distance(ld_state(&s_st[k]));
+                if (!dom) s_tie = 1;
+                continue;
+            }
+            if (sj != ST_KEPT) continue;
             const double hj = s_mh[j];
             double lmin = INF, rmin = INF;
             /* the two walks step together, and a step reads every candidate
@@ -987,7 +1022,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
                 }
             }
             const double prom = hj - fmax(lmin, rmin);
-            st_state(&s_st[j], thr <= prom ? ST_FINAL : ST_REMOVED);
+            st_state(&s_st[j], thr <= prom ? ST_FINAL : ST_PREMOVED);
         }
     }
     __syncthreads();
@@ -1007,6 +1042,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     if (tid == 0) {
         A.nout[f] = w;
         if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
+        if (s_tie && A.flags) A.flags[f] |= A.tie_bit;
     }
     STAMP(5);
     STAMP_FLUSH(A.stamps);

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_fill(PeakArgs A, FplArgs L) {
         const double xv = sg * e[p];
         mp[off + t] = p;
         mh[off + t] = xv;
-        st[off + t] = (!h || h[p] <= xv) ? open : ST_REMOVED;   /* height filter */
+        st[off + t] = (!h || h[p] <= xv) ? open : ST_HEIGHT;    /* height filter */
     }
     /* maxima and valleys alternate (k_find_peaks_lds): the unit's valley t
      * has t of its maxima before it, plus one when its first extremum is one */
@@ -455,7 +455,24 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_prom(PeakArgs A, FplArgs L) {
     if (j >= M) return;
     const int64_t d0 = A.doff[f];
     uint8_t *st = A.state + d0;
-    if (st[j] != ST_KEPT) return;
+    const uint8_t sj = st[j];
+    if (sj == ST_REMOVED && A.distance > 1) {
+        /* removed by the distance filter: a decisive tie (include/bpmx.h
+         * BPMX_F_*_TIE) unless a strictly higher candidate the filter kept lies
+         * within distance (kept states are odd whatever the prominence did) */
+        const int32_t *mp = L.mp + d0;
+        const double *mh = L.mh + d0;
+        const int64_t pj = mp[j], dist = A.distance;
+        const double vj = mh[j];
+        bool dom = false;
+        for (int k = j - 1; !dom && k >= 0 && pj - mp[k] < dist; --k)
+            dom = mh[k] > vj && st_kept_by_distance(__hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        for (int k = j + 1; !dom && k < M && mp[k] - pj < dist; ++k)
+            dom = mh[k] > vj && st_kept_by_distance(__hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (!dom && A.flags) atomicOr(&A.flags[f], A.tie_bit);
+        return;
+    }
+    if (sj != ST_KEPT) return;
     const double *mh = L.mh + d0, *vv = L.vv + d0 + f;
     const int64_t o32 = fpl_b32_off(d0, f), o1k = fpl_b1k_off(d0, f);
     const double *b32h = L.b32h + o32, *b32l = L.b32l + o32, *b32r = L.b32r + o32;
@@ -500,7 +517,8 @@ __global__ __launch_bounds__(FPL_T) void k_fpl_prom(PeakArgs A, FplArgs L) {
     }
     const double prom = hj - fmax(lmin, rmin);
     const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
-    st[j] = thr <= prom ? ST_FINAL : ST_REMOVED;
+    __hip_atomic_store(&st[j], (uint8_t)(thr <= prom ? ST_FINAL : ST_PREMOVED), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(1024) void k_fpl_compact(PeakArgs A, FplArgs L) {

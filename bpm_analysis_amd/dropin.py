@@ -49,6 +49,18 @@ def _file_error(flags: int, params: Dict, sr: int):
     return None
 
 
+TIE_MSG = ("find_peaks' distance filter met equal-height {what} closer than `distance`: numpy's argsort order "
+           "for equal heights is implementation-defined, so these {what} may differ from the reference's on "
+           "this machine (bpmx keeps the later index).")
+
+
+def _warn_ties(flags: int, what: str) -> None:
+    """Report a decisive tie (include/bpmx.h BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE)."""
+    bit = N.F_TROUGH_TIE if what == "troughs" else N.F_PEAK_TIE
+    if flags & bit:
+        logging.warning(TIE_MSG.format(what=what))
+
+
 def _read_wav(file_path: str):
     from scipy.io import wavfile
     with warnings.catch_warnings():
@@ -119,8 +131,17 @@ def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: 
         raise ValueError(PADLEN_MSG)
     _last.rec = None
     stages = N.STAGE_ALL if d.distance >= 1 else N.STAGE_ENVELOPE     # distance < 1 raises in the later calls
-    r = default_detector(device).run_host([audio], sample_rate, params, mode=mode, stages=stages,
-                                          want_y=bool(save_debug_file))[0]
+    det = default_detector(device)
+    try:
+        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file))[0]
+    except N.BpmxError as exc:
+        if stages == N.STAGE_ENVELOPE or not exc.per_file:
+            raise
+        # a detection-stage limit (e.g. a noise window beyond the kernels): the
+        # envelope alone now, so the error surfaces from the floor call as in
+        # the reference (:1732), after the debug WAV is written
+        stages = N.STAGE_ENVELOPE
+        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file))[0]
     if save_debug_file:
         _write_debug_wav(f"{os.path.splitext(file_path)[0]}_filtered_debug.wav", d.sr, r["y"])
         base = os.path.basename(os.path.splitext(file_path)[0])
@@ -149,6 +170,7 @@ def _calculate_dynamic_noise_floor(audio_envelope: np.ndarray, sample_rate: int,
     fl = r["flags"]
     if fl & N.F_BAD_WINDOW:
         raise _window_error(params, sample_rate)
+    _warn_ties(fl, "troughs")
     if fl & N.F_STATIC_FLOOR:
         logging.warning("Not enough troughs found for sanitization. Using a static noise floor.")
         return _series(np.array(r["floor"])), np.array(r["troughs"], dtype=np.int64)
@@ -170,6 +192,7 @@ def find_raw_peaks(audio_envelope: np.ndarray, sample_rate: int, params: Dict, h
     if r is None or not _same_bytes(r["floor"], floor):
         r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor])[0]
     peaks = np.array(r["peaks"], dtype=np.int64)
+    _warn_ties(r["flags"], "peaks")
     logging.info(f"Found {len(peaks)} raw peaks using dynamic height threshold.")
     return peaks
 

@@ -67,8 +67,19 @@ enum bpmx_file_flag {
     BPMX_F_DRAFT_FLOOR = 2,  /* <= 2 sanitised troughs: draft floor kept (:1107-1110) */
     BPMX_F_NAN_FLOOR = 4,    /* all-NaN floor replaced by quantile(env, 0.1) (:1113-1115) */
     BPMX_F_TOO_SHORT = 8,    /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
-    BPMX_F_BAD_WINDOW = 16   /* noise_window < min_periods and >= 5 troughs: pandas rolling() raises
+    BPMX_F_BAD_WINDOW = 16,  /* noise_window < min_periods and >= 5 troughs: pandas rolling() raises
                                 ValueError (:1085); floor/peaks of this recording are not meaningful */
+    /* find_peaks' distance filter visits candidates in np.argsort(height) order
+     * (scipy/signal/_peak_finding.py:976-978), which is unstable: for equal
+     * heights the order is numpy's implementation detail (x86-simd-sort on
+     * AVX-512, introsort elsewhere).  bpmx keeps the stable order (the later
+     * index first among equals) and sets these bits exactly when that choice
+     * decided a removal: some candidate was removed by an equal-height kept one
+     * with no strictly higher kept one within `distance`.  Without the bit the
+     * indices are those of every argsort order, so the reference's; with it
+     * they may differ from the reference's on that machine. */
+    BPMX_F_TROUGH_TIE = 32,  /* in the trough search find_peaks(-env) (:1070) */
+    BPMX_F_PEAK_TIE = 64     /* in the raw-peak search find_peaks(env, height=floor) (:227) */
 };
 
 enum bpmx_option {

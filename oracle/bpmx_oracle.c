@@ -339,8 +339,21 @@ double bpmo_quantile(const double *x, int64_t n, double q) {
 /*   keep-highest in argsort order), _peak_prominences (wlen=-1).            */
 /* x is read as sgn*v so troughs (find_peaks(-env)) need no copy.            */
 /* Ties of priority in the distance filter: numpy's default argsort is not   */
-/* stable (its order is implementation-defined); this restatement uses the   */
-/* stable order, i.e. among equal heights the later peak is visited first.   */
+/* stable (its order is implementation-defined: x86-simd-sort on AVX-512,     */
+/* introsort elsewhere); this restatement uses the stable order, i.e. among  */
+/* equal heights the later peak is visited first, and reports whether that   */
+/* choice decided anything (*tie, below).                                     */
+/*                                                                            */
+/* When is the tie order decisive?  _select_by_peak_distance visits the      */
+/* candidates in priority blocks of equal height, highest first; a candidate */
+/* is still alive when its block starts iff no KEPT candidate of strictly    */
+/* greater height lies within `distance`.  If two alive candidates of one    */
+/* block lie within `distance`, whichever is visited first removes the      */
+/* other, so the order decides the outcome; otherwise no order can change    */
+/* it.  In terms of the finished stable pass (by induction from the highest  */
+/* block, whose alive set no order can change): the order was decisive iff   */
+/* some REMOVED candidate has no kept candidate of strictly greater height   */
+/* within `distance` — it was removed by an equal-height one.                */
 /* ------------------------------------------------------------------------ */
 typedef struct { double p; int64_t i; } prio_t;
 static int cmp_prio(const void *pa, const void *pb) {
@@ -350,8 +363,22 @@ static int cmp_prio(const void *pa, const void *pb) {
     return (a->i > b->i) - (a->i < b->i);
 }
 
-int64_t bpmo_find_peaks(const double *v, int64_t n, double sgn, const double *height, int64_t distance,
-                        double prominence, int64_t *out) {
+/* _peak_prominences with wlen = -1 (scipy/signal/_peak_finding.py:982-995 ->
+ * _peak_finding_utils): walk left while x <= x[p] tracking the minimum, the
+ * same to the right; prominence = x[p] - max(left min, right min) */
+double bpmo_prominence(const double *v, int64_t n, double sgn, int64_t p) {
+    double xp = sgn * v[p];
+    double lmin = xp, rmin = xp;
+    for (int64_t k = p; k >= 0 && sgn * v[k] <= xp; --k)
+        if (sgn * v[k] < lmin) lmin = sgn * v[k];
+    for (int64_t k = p; k <= n - 1 && sgn * v[k] <= xp; ++k)
+        if (sgn * v[k] < rmin) rmin = sgn * v[k];
+    return xp - (lmin > rmin ? lmin : rmin);
+}
+
+int64_t bpmo_find_peaks_ex(const double *v, int64_t n, double sgn, const double *height, int64_t distance,
+                           double prominence, int64_t *out, int *tie) {
+    if (tie) *tie = 0;
 #define X(k) (sgn * v[(k)])
     int64_t *pk = (int64_t *)malloc(sizeof(int64_t) * (n / 2 + 2));
     int64_t m = 0;
@@ -387,6 +414,16 @@ int64_t bpmo_find_peaks(const double *v, int64_t n, double sgn, const double *he
             for (int64_t k = j - 1; k >= 0 && pk[j] - pk[k] < distance; --k) keep[k] = 0;
             for (int64_t k = j + 1; k < m && pk[k] - pk[j] < distance; ++k) keep[k] = 0;
         }
+        /* decisive tie: a removed candidate with no strictly higher kept one in reach */
+        for (int64_t j = 0; j < m && tie && !*tie; ++j) {
+            if (keep[j]) continue;
+            int dominated = 0;
+            for (int64_t k = j - 1; k >= 0 && pk[j] - pk[k] < distance && !dominated; --k)
+                dominated = keep[k] && X(pk[k]) > X(pk[j]);
+            for (int64_t k = j + 1; k < m && pk[k] - pk[j] < distance && !dominated; ++k)
+                dominated = keep[k] && X(pk[k]) > X(pk[j]);
+            if (!dominated) *tie = 1;
+        }
         int64_t w = 0;
         for (int64_t j = 0; j < m; ++j)
             if (keep[j]) pk[w++] = pk[j];
@@ -397,23 +434,19 @@ int64_t bpmo_find_peaks(const double *v, int64_t n, double sgn, const double *he
     /* prominence (wlen = -1: whole signal) */
     if (!isnan(prominence)) {
         int64_t w = 0;
-        for (int64_t j = 0; j < m; ++j) {
-            int64_t p = pk[j];
-            double xp = X(p);
-            double lmin = xp, rmin = xp;
-            for (int64_t k = p; k >= 0 && X(k) <= xp; --k)
-                if (X(k) < lmin) lmin = X(k);
-            for (int64_t k = p; k <= n - 1 && X(k) <= xp; ++k)
-                if (X(k) < rmin) rmin = X(k);
-            double prom = xp - (lmin > rmin ? lmin : rmin);
-            if (prominence <= prom) pk[w++] = p;
-        }
+        for (int64_t j = 0; j < m; ++j)
+            if (prominence <= bpmo_prominence(v, n, sgn, pk[j])) pk[w++] = pk[j];
         m = w;
     }
 #undef X
     if (out) memcpy(out, pk, sizeof(int64_t) * m);
     free(pk);
     return m;
+}
+
+int64_t bpmo_find_peaks(const double *v, int64_t n, double sgn, const double *height, int64_t distance,
+                        double prominence, int64_t *out) {
+    return bpmo_find_peaks_ex(v, n, sgn, height, distance, prominence, out, NULL);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -519,6 +552,8 @@ void bpmo_rolling_quantile(const double *v, int64_t n, int64_t w, int64_t minp, 
 /* flags bit0: static fallback (<5 troughs, :1073-1077)                       */
 /*       bit1: sanitized <= 2, draft floor kept (:1107-1110)                  */
 /*       bit2: all-NaN floor -> quantile(env, 0.1) (:1113-1115)               */
+/*       bit5: the trough search's distance filter met a decisive height tie  */
+/*             (bpmo_find_peaks_ex; BPMX_F_TROUGH_TIE in include/bpmx.h)      */
 /* Returns the number of troughs written (sanitized, or raw in bit0 case).   */
 /* ------------------------------------------------------------------------ */
 typedef struct {
@@ -536,7 +571,9 @@ int64_t bpmo_noise_floor(const double *env, int64_t n, const bpmo_nf_params *p, 
     *flags = 0;
     double qt = bpmo_quantile(env, n, p->trough_prom_q);
     int64_t *tr = (int64_t *)malloc(sizeof(int64_t) * (n / 2 + 2));
-    int64_t nt = bpmo_find_peaks(env, n, -1.0, NULL, p->distance, qt, tr);
+    int tie = 0;
+    int64_t nt = bpmo_find_peaks_ex(env, n, -1.0, NULL, p->distance, qt, tr, &tie);
+    if (tie) *flags |= 32;
     if (nt < 5) {
         double fb = bpmo_quantile(env, n, p->noise_floor_q);
         for (int64_t i = 0; i < n; ++i) floor_out[i] = fb;
@@ -575,9 +612,15 @@ int64_t bpmo_noise_floor(const double *env, int64_t n, const bpmo_nf_params *p, 
     return ns;
 }
 
-/* A12: PeakClassifier._find_raw_peaks (bpm_analysis.py:223-229) */
+/* A12: PeakClassifier._find_raw_peaks (bpm_analysis.py:223-229); *tie (may be
+ * NULL) = the distance filter met a decisive height tie (BPMX_F_PEAK_TIE) */
+int64_t bpmo_raw_peaks_ex(const double *env, int64_t n, const double *floor_v, int64_t distance,
+                          double peak_prom_q, int64_t *out, int *tie) {
+    double qp = bpmo_quantile(env, n, peak_prom_q);
+    return bpmo_find_peaks_ex(env, n, 1.0, floor_v, distance, qp, out, tie);
+}
+
 int64_t bpmo_raw_peaks(const double *env, int64_t n, const double *floor_v, int64_t distance, double peak_prom_q,
                        int64_t *out) {
-    double qp = bpmo_quantile(env, n, peak_prom_q);
-    return bpmo_find_peaks(env, n, 1.0, floor_v, distance, qp, out);
+    return bpmo_raw_peaks_ex(env, n, floor_v, distance, peak_prom_q, out, NULL);
 }

@@ -59,6 +59,12 @@ def lib() -> ctypes.CDLL:
         L.bpmo_quantile.restype = D
         L.bpmo_find_peaks.argtypes = [P, I64, D, P, I64, D, P]
         L.bpmo_find_peaks.restype = I64
+        L.bpmo_find_peaks_ex.argtypes = [P, I64, D, P, I64, D, P, ctypes.POINTER(I)]
+        L.bpmo_find_peaks_ex.restype = I64
+        L.bpmo_prominence.argtypes = [P, I64, D, I64]
+        L.bpmo_prominence.restype = D
+        L.bpmo_raw_peaks_ex.argtypes = [P, I64, P, I64, D, P, ctypes.POINTER(I)]
+        L.bpmo_raw_peaks_ex.restype = I64
         L.bpmo_noise_floor.argtypes = [P, I64, P, P, P, ctypes.POINTER(I)]
         L.bpmo_noise_floor.restype = I64
         L.bpmo_raw_peaks.argtypes = [P, I64, P, I64, D, P]
@@ -188,13 +194,71 @@ def quantile(x: np.ndarray, q: float) -> float:
     return lib().bpmo_quantile(_p(x), x.size, q)
 
 
-def find_peaks(x: np.ndarray, height=None, distance: int = 0, prominence=None, negate: bool = False) -> np.ndarray:
+# per-file flag bits of the decisive-tie report (include/bpmx.h BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE)
+F_TROUGH_TIE = 32
+F_PEAK_TIE = 64
+
+
+def find_peaks(x: np.ndarray, height=None, distance: int = 0, prominence=None, negate: bool = False,
+               return_tie: bool = False):
+    """scipy.signal.find_peaks(sign*x, height, distance, prominence) with the stable
+    tie order (bpmx_oracle.c); with return_tie also whether that order decided
+    anything in the distance filter (see bpmo_find_peaks_ex)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     out = np.empty(x.size // 2 + 2, dtype=np.int64)
     h = None if height is None else np.ascontiguousarray(height, dtype=np.float64)
-    m = lib().bpmo_find_peaks(_p(x), x.size, -1.0 if negate else 1.0, None if h is None else _p(h),
-                              distance, np.nan if prominence is None else float(prominence), _p(out))
-    return out[:m].copy()
+    tie = ctypes.c_int(0)
+    m = lib().bpmo_find_peaks_ex(_p(x), x.size, -1.0 if negate else 1.0, None if h is None else _p(h),
+                                 distance, np.nan if prominence is None else float(prominence), _p(out),
+                                 ctypes.byref(tie))
+    pk = out[:m].copy()
+    return (pk, bool(tie.value)) if return_tie else pk
+
+
+def find_peaks_numpy_order(x: np.ndarray, height=None, distance: int = 0, prominence=None,
+                           negate: bool = False) -> np.ndarray:
+    """find_peaks with the distance filter visiting numpy's default argsort
+    order, as the reference's own call does on this machine: local maxima and
+    height from bpmx_oracle.c, the distance filter by select_by_peak_distance,
+    prominences by bpmo_prominence.  Pins the stable-order restatement on tie
+    inputs (tests/test_oracle.py); small cases only."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    sg = -1.0 if negate else 1.0
+    cand = find_peaks(x, height=height, negate=negate)
+    if distance and cand.size:
+        cand = cand[select_by_peak_distance(cand, sg * x[cand], distance, "numpy")]
+    if prominence is not None:
+        cand = np.array([p for p in cand if float(prominence) <= lib().bpmo_prominence(_p(x), x.size, sg, int(p))],
+                        dtype=np.int64)
+    return cand
+
+
+def select_by_peak_distance(peaks: np.ndarray, priority: np.ndarray, distance: int, order: str = "numpy"):
+    """scipy _peak_finding_utils._select_by_peak_distance restated in Python
+    (scipy/signal/_peak_finding.py:976-980 calls it; its loop: visit
+    ``np.argsort(priority)`` from the end, a kept peak removes every peak
+    closer than ceil(distance) on both sides).  ``order="numpy"`` takes
+    numpy's default (unstable) argsort exactly as the reference does, on this
+    machine's numpy; ``"stable"`` is the convention of bpmx_oracle.c and the
+    kernels.  Pure-Python loop: small cases only (tie pinning tests)."""
+    peaks = np.asarray(peaks, dtype=np.int64)
+    pr = np.asarray(priority, dtype=np.float64)
+    d = int(np.ceil(distance))
+    keep = np.ones(peaks.size, dtype=bool)
+    idx = np.argsort(pr) if order == "numpy" else np.argsort(pr, kind="stable")
+    for i in range(peaks.size - 1, -1, -1):
+        j = int(idx[i])
+        if not keep[j]:
+            continue
+        k = j - 1
+        while k >= 0 and peaks[j] - peaks[k] < d:
+            keep[k] = False
+            k -= 1
+        k = j + 1
+        while k < peaks.size and peaks[k] - peaks[j] < d:
+            keep[k] = False
+            k += 1
+    return keep
 
 
 def interp_dense(troughs: np.ndarray, env: np.ndarray) -> np.ndarray:
@@ -226,12 +290,14 @@ def noise_floor(env: np.ndarray, d: Derived, params: dict):
     return floor, tr[:m].copy(), flags.value
 
 
-def raw_peaks(env: np.ndarray, floor: np.ndarray, d: Derived, params: dict) -> np.ndarray:
+def raw_peaks(env: np.ndarray, floor: np.ndarray, d: Derived, params: dict, return_tie: bool = False):
     env = np.ascontiguousarray(env, dtype=np.float64)
     floor = np.ascontiguousarray(floor, dtype=np.float64)
     out = np.empty(env.size // 2 + 2, dtype=np.int64)
-    m = lib().bpmo_raw_peaks(_p(env), env.size, _p(floor), d.distance, params["peak_prominence_quantile"], _p(out))
-    return out[:m].copy()
+    tie = ctypes.c_int(0)
+    m = lib().bpmo_raw_peaks_ex(_p(env), env.size, _p(floor), d.distance, params["peak_prominence_quantile"],
+                                _p(out), ctypes.byref(tie))
+    return (out[:m].copy(), bool(tie.value)) if return_tie else out[:m].copy()
 
 
 def detect(pcm: np.ndarray, fs: int, params: dict, mode: str = "reference"):
@@ -242,5 +308,6 @@ def detect(pcm: np.ndarray, fs: int, params: dict, mode: str = "reference"):
     else:
         env, y = preprocess_native(pcm, d, return_y=True)
     floor, troughs, flags = noise_floor(env, d, params)
-    peaks = raw_peaks(env, floor, d, params)
+    peaks, ptie = raw_peaks(env, floor, d, params, return_tie=True)
+    flags |= F_PEAK_TIE if ptie else 0
     return dict(env=env, y=y, floor=floor, troughs=troughs, peaks=peaks, sr=d.sr, flags=flags)

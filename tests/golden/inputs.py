@@ -148,4 +148,60 @@ def env_cases() -> dict:
     out["env_random_long_window"] = (r, sr, dict(noise_window_sec=20))
     r2 = np.abs(np.convolve(rng.standard_normal(9000), np.ones(9) / 9.0, mode="same")) * 100.0 + 1.0
     out["env_random_rough"] = (r2, sr, None)
+    out.update(tie_env_cases())
     return out
+
+
+def _tie_pairs(seed: int, n_groups: int = 100) -> np.ndarray:
+    """Piecewise-linear envelope whose local maxima come in pairs closer than
+    find_peaks' distance (15 samples at 302 Hz), and whose minima (the troughs
+    find_peaks(-env) sees) come in pairs too.  Within a pair both extrema sit
+    on integer knots, and in three groups of four their values are exactly
+    equal: the distance filter then meets two equal priorities, and
+    numpy's argsort (bpm_analysis.py:1070, :227 -> scipy _peak_finding.py:976-978)
+    decides which one stays."""
+    h = _hash_u32(seed, 8 * n_groups).astype(np.int64)
+    pos, val = [0], [60.0]
+    x = 12
+    for g in range(n_groups):
+        u = h[8 * g: 8 * g + 8]
+        hp = 400 + 10 * int(u[0] % 40)                    # peak pair height
+        hp2 = hp if u[1] % 4 else hp + 1 + int(u[1] % 7)  # equal in 3 of 4 groups
+        sep = 4 + int(u[2] % 10)                          # 4..13 samples apart
+        dip = hp - 40 - int(u[3] % 120)
+        lo = 20 + int(u[4] % 25)                          # trough pair depth
+        lo2 = lo if u[5] % 4 else lo + 1 + int(u[5] % 5)
+        tsep = 4 + int(u[6] % 10)
+        bump = lo + 15 + int(u[7] % 30)
+        pos += [x, x + sep // 2, x + sep]
+        val += [float(hp), float(dip), float(hp2)]
+        x += sep + 9 + int(u[0] % 7)
+        pos += [x, x + tsep // 2, x + tsep]
+        val += [float(lo), float(bump), float(lo2)]
+        x += tsep + 9 + int(u[3] % 7)
+    pos.append(x + 10)
+    val.append(60.0)
+    return _vshape(np.array(pos), np.array(val), x + 11)
+
+
+def _quantized_labeler_env(seed: int, secs: int = 40) -> np.ndarray:
+    """The labeler's envelope recipe (heartbeat_labeler.py:63-67: centred
+    rolling mean of |x| over sr // 10 samples) on coarsely quantized and
+    clipped PCM: the synthetic recording picked at 302 Hz, shifted down to
+    small integers and clipped at +-12, so every envelope value is k / 30 and
+    equal-height extrema within `distance` are common."""
+    x = _synth(seed, secs * 44100, 44100, 1)[::146].astype(np.int64)
+    q = np.clip(x >> 9, -12, 12).astype(np.float64)
+    import pandas as pd
+    return pd.Series(np.abs(q)).rolling(window=30, min_periods=1, center=True).mean().values
+
+
+def tie_env_cases() -> dict:
+    """Envelopes with exact height ties inside find_peaks' distance filter, for
+    the decisive-tie report (BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE)."""
+    sr = 302
+    return {
+        "env_ties_pairs": (_tie_pairs(41), sr, None),
+        "env_ties_quantized": (_quantized_labeler_env(42), sr, None),
+        "env_ties_quantized_b": (_quantized_labeler_env(43, 60), sr, dict(trough_rejection_multiplier=2.0)),
+    }

@@ -129,9 +129,18 @@ def make_env_case(name, env, sr, over=None):
     params = _params(over)
     env = np.ascontiguousarray(env, dtype=np.float64)
     floor, troughs, peaks, fl = _floor_and_peaks(env, sr, params)
+    extra = {}
+    if name.startswith("env_ties"):
+        # the raw troughs before sanitisation, by the reference's own call
+        # (bpm_analysis.py:1066-1070), so the tie tests can pin the trough
+        # search separately from the floor
+        from scipy.signal import find_peaks
+        d = int(params["min_peak_distance_sec"] * sr)
+        q = np.quantile(env, params["trough_prominence_quantile"])
+        extra["raw_troughs"] = find_peaks(-env, distance=d, prominence=q)[0].astype(np.int64)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), kind="env", mode="env", sr=sr, fs=sr,
                         params=json.dumps({k: params[k] for k in HOT_KEYS}), env=env, floor=floor,
-                        troughs=troughs, peaks=peaks, flags=fl)
+                        troughs=troughs, peaks=peaks, flags=fl, **extra)
     print(f"{name:28s} env-level sr={sr} Nd={len(env)} troughs={len(troughs)} peaks={len(peaks)} flags={fl}")
 
 
@@ -158,15 +167,21 @@ def make_vulpine():
     print(f"vulpine: log peaks={len(peaks)} log troughs={len(troughs)}; pipeline troughs={len(tr)} peaks={len(pk)}")
 
 
-def main():
+def main(only=None):
+    """Every fixture, or only those whose names start with one of `only`
+    (e.g. ``python tests/golden/make_goldens.py env_ties``)."""
     np.seterr(all="ignore")
     logging.getLogger().setLevel(logging.WARNING)
+    want = (lambda n: any(n.startswith(o) for o in only)) if only else (lambda n: True)
     for name, spec, mode, over, store in I.CASES:
-        make_pcm_case(name, spec, mode, over, store)
+        if want(name):
+            make_pcm_case(name, spec, mode, over, store)
     for name, (env, sr, over) in I.env_cases().items():
-        make_env_case(name, env, sr, over)
-    make_vulpine()
+        if want(name):
+            make_env_case(name, env, sr, over)
+    if want("vulpine"):
+        make_vulpine()
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -15,16 +15,30 @@ BASE_PARAMS = {"downsample_factor": 300, "save_filtered_wav": False, "min_peak_d
                "noise_floor_quantile": 0.20, "noise_window_sec": 10, "trough_rejection_multiplier": 4.0}
 
 
-def names(kind=None, mode=None):
+def names(kind=None, mode=None, prefix=None):
     out = []
     for p in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
+        name = os.path.splitext(os.path.basename(p))[0]
+        if prefix and not name.startswith(prefix):
+            continue
         with np.load(p, allow_pickle=False) as z:
             if kind and str(z["kind"]) != kind:
                 continue
             if mode and str(z["mode"]) != mode:
                 continue
-        out.append(os.path.splitext(os.path.basename(p))[0])
+        out.append(name)
     return out
+
+
+def env_derived(g):
+    """oracle.Derived for an env-level fixture (only sr / distance / noise window matter)."""
+    from oracle import oracle as O
+    d = O.derive(302 * 146, dict(g["params"]))
+    sr = int(g["sr"])
+    d.sr = sr
+    d.distance = int(g["params"]["min_peak_distance_sec"] * sr)
+    d.noise_window = int(g["params"]["noise_window_sec"] * sr)
+    return d
 
 
 def load(name):

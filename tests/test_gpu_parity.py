@@ -32,7 +32,19 @@ def _check_file(r, g, exact_env=True):
         assert np.allclose(r["floor"], g["floor"], rtol=1e-9, atol=1e-9 * scale)
     assert _same(r["troughs"], g["troughs"])
     assert _same(r["peaks"], g["peaks"])
-    assert (r["flags"] & 7) == int(g["flags"])
+    _check_flags(r["flags"], int(g["flags"]))
+
+
+FALLBACK_BITS = 3      # the flags the reference's log lines pin (static / draft fallback, :1074, :1109)
+TIE_BITS = O.F_TROUGH_TIE | O.F_PEAK_TIE
+
+
+def _check_flags(got, want):
+    """Both sides masked the same way: the fallback bits equal, and no decisive
+    find_peaks tie on an input the reference's output pins (tie cases have
+    their own test)."""
+    assert (got & FALLBACK_BITS) == (want & FALLBACK_BITS)
+    assert got & TIE_BITS == 0
 
 
 def test_device_synth_matches_host(det):
@@ -71,7 +83,7 @@ def test_ragged_batch_matches_single(det):
         assert r["n_raw_troughs"] == len(O.find_peaks(g["env"], distance=d.distance, prominence=prom, negate=True))
 
 
-@pytest.mark.parametrize("name", G.names(kind="env"))
+@pytest.mark.parametrize("name", [n for n in G.names(kind="env") if not n.startswith("env_ties")])
 def test_env_level_golden(det, name):
     from bpm_analysis_amd import _native as N
     g = G.load(name)
@@ -79,9 +91,47 @@ def test_env_level_golden(det, name):
     r = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR)[0]
     assert _same(r["floor"], g["floor"])
     assert _same(r["troughs"], g["troughs"])
-    assert (r["flags"] & 7) == int(g["flags"])
+    _check_flags(r["flags"], int(g["flags"]))
     p = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_PEAKS, floors=[g["floor"]])[0]
     assert _same(p["peaks"], g["peaks"])
+    assert p["flags"] & TIE_BITS == 0
+
+
+@pytest.mark.parametrize("name", G.names(kind="env", prefix="env_ties"))
+def test_tie_goldens_flagged(det, name):
+    """Equal-height extrema within find_peaks' distance (reference-made goldens:
+    pairs of equal maxima / minima, the labeler envelope of quantized PCM).
+    The kernels keep the stable order, so they equal the oracle; they set
+    BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE exactly where the oracle does, and
+    wherever the reference's (numpy argsort) answer differs from theirs."""
+    from bpm_analysis_amd import _native as N
+    g = G.load(name)
+    sr = int(g["sr"])
+    d = G.env_derived(g)
+    of, ot, ofl = O.noise_floor(g["env"], d, g["params"])
+    r = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR)[0]
+    assert _same(r["floor"], of) and _same(r["troughs"], ot)
+    assert r["flags"] == ofl
+    assert r["flags"] & N.F_TROUGH_TIE
+    assert r["n_raw_troughs"] == len(O.find_peaks(g["env"], distance=d.distance, negate=True,
+                                                  prominence=O.quantile(g["env"], g["params"]["trough_prominence_quantile"])))
+    raw = O.find_peaks(g["env"], distance=d.distance, negate=True,
+                       prominence=O.quantile(g["env"], g["params"]["trough_prominence_quantile"]))
+    assert not _same(raw, g["raw_troughs"])           # the tie order decided something here
+    # peaks on the reference's own floor: flagged, equal to the oracle's stable answer
+    p = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_PEAKS, floors=[g["floor"]])[0]
+    opk, otie = O.raw_peaks(g["env"], g["floor"], d, g["params"], return_tie=True)
+    assert _same(p["peaks"], opk)
+    assert bool(p["flags"] & N.F_PEAK_TIE) == otie
+    if not otie:
+        assert _same(p["peaks"], g["peaks"])
+    # the same envelopes through the long-recording kernels (k_fpl_*) and the
+    # one-workgroup global-memory kernel: same outputs and flags
+    for opt in (N.OPT_PEAKS_GLOBAL,):
+        r2 = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR, options=opt)[0]
+        assert _same(r2["troughs"], ot) and r2["flags"] == ofl
+        p2 = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_PEAKS, floors=[g["floor"]], options=opt)[0]
+        assert _same(p2["peaks"], opk) and p2["flags"] == p["flags"]
 
 
 def test_vulpine_reference_pipeline_and_known_answer(det):
@@ -89,10 +139,12 @@ def test_vulpine_reference_pipeline_and_known_answer(det):
     g = G.load("vulpine")
     r = det.run_host([g["pcm"]], int(g["fs"]), g["params"], mode="reference")[0]
     _check_file(r, g)
-    # labeler-recipe envelope (heartbeat_labeler.py:63-67) -> every Debug_Log raw peak
+    # labeler-recipe envelope (heartbeat_labeler.py:63-67) -> every Debug_Log raw peak;
+    # its trough search meets a decisive tie (int16 |x| means are multiples of 1/30)
     env = O.rolling_mean(np.abs(g["pcm"]).astype(np.float64), int(g["fs"]) // 10, 1)
     fl = det.run_env_host([env], 302, g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS)[0]
     assert _same(fl["peaks"], g["log_peaks"])
+    assert fl["flags"] & TIE_BITS == N.F_TROUGH_TIE
     assert len(np.intersect1d(fl["troughs"], g["log_troughs"])) >= 1345
 
 
@@ -361,6 +413,8 @@ def test_find_peaks_kernels_agree(det):
         assert _same(x["troughs"], y["troughs"])
         assert _same(x["peaks"], y["peaks"])
         assert _same(x["floor"], y["floor"])
+        assert x["flags"] == y["flags"]                 # decisive-tie reports included
+    assert any(x["flags"] & TIE_BITS for x in a)
     # with recordings beyond 65536 samples in the batch, the long ones and the
     # short ones with > 3072 maxima take the multi-workgroup k_fpl_* path
     m = 200_000
@@ -382,10 +436,15 @@ def test_find_peaks_kernels_agree(det):
         assert _same(x["troughs"], y["troughs"])
         assert _same(x["peaks"], y["peaks"])
         assert _same(x["floor"], y["floor"])
+        assert x["flags"] == y["flags"]
     d = O.derive(302, params)
-    of, ot, _ = O.noise_floor(long_envs[0], d, params)
-    assert _same(a[0]["troughs"], ot)
-    assert _same(a[0]["peaks"], O.raw_peaks(long_envs[0], of, d, params))
+    for k in (0, 2):                   # 2: ties everywhere, through k_fpl_prom's tie check
+        of, ot, ofl = O.noise_floor(long_envs[k], d, params)
+        opk, ptie = O.raw_peaks(long_envs[k], of, d, params, return_tie=True)
+        assert _same(a[k]["troughs"], ot)
+        assert _same(a[k]["peaks"], opk)
+        assert a[k]["flags"] == ofl | (O.F_PEAK_TIE if ptie else 0)
+    assert a[2]["flags"] & TIE_BITS
 
 
 @pytest.mark.parametrize("fs", [44100, 22050, 48000])
@@ -461,7 +520,7 @@ def test_draft_bounds_match_full_draft(det, name):
         r = det.run_env_host([g["env"]], int(g["sr"]), g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS, options=opt)[0]
         assert _same(r["floor"], g["floor"])
         assert _same(r["troughs"], g["troughs"])
-        assert (r["flags"] & 7) == int(g["flags"])
+        _check_flags(r["flags"], int(g["flags"]))
         assert _same(r["peaks"], g["peaks"])
 
 
@@ -845,7 +904,7 @@ def test_draft_point_resolves_undecided_troughs(det, mult):
         assert a["flags"] == b["flags"]
         d = O.derive(sr, params)
         of, ot, ofl = O.noise_floor(env, d, params)
-        assert _same(a["floor"], of) and _same(a["troughs"], ot) and (a["flags"] & 7) == ofl
+        assert _same(a["floor"], of) and _same(a["troughs"], ot) and (a["flags"] & ~O.F_PEAK_TIE) == ofl
     assert raw > 0
     if mult <= 2.0:
         assert und > 0.05 * raw            # the pointwise path is really exercised

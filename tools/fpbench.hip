@@ -66,6 +66,7 @@ int main(int argc, char **argv) {
         a.bmin = d_bmn; a.qv = d_qv; a.qslot = sg < 0 ? Q_TROUGH : Q_PEAK; a.n_files = (int)F; a.distance = 15;
         a.sign = sg; a.cand = d_cand; a.state = d_state; a.out = d_out; a.nout = d_nout; a.run_out = nullptr;
         a.run_min = 0; a.stamps = d_st; a.vcand = d_vc; a.fallback = d_fb; a.only = nullptr; a.lds_nmax = INT64_MAX;
+        a.flags = nullptr; a.tie_bit = 0;
         const bool lds = argc > 2 && argv[2][0] == 'l';
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
