@@ -44,7 +44,11 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="native", choices=["native", "reference"])
-    ap.add_argument("--files", type=int, default=1024, help="recordings per GPU")
+    ap.add_argument("--files", type=int, default=1024, help="recordings per GPU (weak scaling, the default line)")
+    ap.add_argument("--files-total", type=int, default=0,
+                    help="strong scaling: this many recordings in the whole job, split evenly over the ranks "
+                         "(BASELINE C4: --gpus 8 --files-total 4096; the metric's 1024-file batch at any N: 1024); "
+                         "0: --files per GPU")
     ap.add_argument("--secs", type=float, default=60.0)
     ap.add_argument("--fs", type=int, default=44100)
     ap.add_argument("--cpu-files", type=int, default=-1, help="CPU baseline sample size (-1: auto, 0: skip)")
@@ -72,8 +76,9 @@ def parse(argv=None):
                          "contexts and streams, so one sub-batch's latency-bound kernels fill another's gaps "
                          "(3: the box's GPU_MAX_HW_QUEUES = 4 leaves three hardware queues beside the null "
                          "stream's; a fourth stream shares one and serialises)")
-    ap.add_argument("--c5-parity-files", type=int, default=2,
-                    help="C5: each rank's shortest recordings checked against the oracle")
+    ap.add_argument("--c5-parity-files", type=int, default=-1,
+                    help="C5: each rank's shortest recordings checked against the oracle (-1: every recording of "
+                         "the rank; ~15 s of 16-thread oracle time per 64 recordings)"),
     ap.add_argument("--dropin-files", type=int, default=3,
                     help="side measurement: per-file latency of the reference's call sequence through the "
                          "drop-in on 60 s WAV files (0: skip)")
@@ -304,6 +309,19 @@ def shard_seed0(rank: int, files_per_gpu: int) -> int:
     return rank * files_per_gpu
 
 
+def shard_files(args, rank: int, world: int):
+    """(first recording index = seed, recordings on this rank, recordings in the job).
+
+    Weak scaling (default): --files per rank, rank r holding r*F .. r*F+F-1.
+    Strong scaling (--files-total T): the job's T equal-length recordings split
+    into contiguous, as-even-as-possible runs (the LPT placement of equal
+    lengths, gui.py:202-251's loop sharded); a rank may hold none."""
+    if args.files_total > 0:
+        lo, hi = rank * args.files_total // world, (rank + 1) * args.files_total // world
+        return lo, hi - lo, args.files_total
+    return shard_seed0(rank, args.files), args.files, world * args.files
+
+
 def reduce_results(elapsed: float, n_peaks, world: int, rank: int):
     """Max wall time over ranks, and the final result gather: every shard's
     per-file raw-peak counts to rank 0 (RCCL on the GPU box, gloo in the CPU
@@ -314,7 +332,7 @@ def reduce_results(elapsed: float, n_peaks, world: int, rank: int):
         return elapsed, int(n_peaks.sum())
     tt = torch.tensor([elapsed], dtype=torch.float64, device=n_peaks.device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    counts = n_peaks.clone()
+    counts = n_peaks.sum(dtype=torch.int64).reshape(1)     # ranks may hold different file counts (--files-total)
     gathered = [torch.empty_like(counts) for _ in range(world)] if rank == 0 else None
     dist.gather(counts, gathered, dst=0)
     total = int(sum(int(g.sum()) for g in gathered)) if rank == 0 else 0
@@ -377,7 +395,8 @@ def run_c5(args):
         t = torch.tensor([n_rounds], dtype=torch.int64, device=det.device if backend == "nccl" else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n_rounds = int(t.item())
-    pick = set(sorted(mine, key=lambda i: lengths[i])[:max(0, args.c5_parity_files)]) if not args.no_cpu else set()
+    npar = len(mine) if args.c5_parity_files < 0 else args.c5_parity_files
+    pick = set(sorted(mine, key=lambda i: lengths[i])[:npar]) if not args.no_cpu else set()
     kept, rows, kprof = {}, [], {}
     frames = nd_tot = 0
     elapsed = 0.0
@@ -566,11 +585,14 @@ def main(args):
     cdev = det.device if backend == "nccl" else None          # collectives' tensors: the GPU under RCCL
     params = dict(DEFAULT_PARAMS)
     params["save_filtered_wav"] = False
-    fs, F = args.fs, args.files
+    fs = args.fs
+    seed0, F, total_files = shard_files(args, rank, world)
+    if F < 1:
+        raise SystemExit(f"bench.py: rank {rank} holds no recording (--files-total {args.files_total} over {world})")
     n = int(round(args.secs * fs))
     d = design(fs, params, log=False)
     fo = np.arange(F + 1, dtype=np.int64) * n
-    pcm = det.synth(fo, fs, 1, seed0=shard_seed0(rank, F))
+    pcm = det.synth(fo, fs, 1, seed0=seed0)
     out = det.alloc(fo, d.ds, d.sr)
     nd = -(-n // d.ds)
 
@@ -740,7 +762,7 @@ def main(args):
         # passes it to every rank); otherwise split the affinity mask over the ranks
         th = th_all if os.environ.get("OMP_NUM_THREADS", "").isdigit() else max(1, th_all // max(1, lw))
         pick = sorted(set(np.linspace(0, F - 1, min(F, args.parity_files)).astype(int).tolist()))
-        seeds = [shard_seed0(rank, F) + f for f in pick]
+        seeds = [seed0 + f for f in pick]
         outs, odt = oracle_outputs(args.mode, fs, n, seeds, params, th)
         pr = compare_outputs([gpu_host[f] for f in pick], outs, exact_env=(args.mode == "reference"))
         cnt = torch.tensor([pr["files"], pr["peaks_equal"], pr["troughs_equal"], pr["flags_equal"]],
@@ -769,7 +791,7 @@ def main(args):
     # 8(e)): raw peaks of every file, and final beats + the smoothed BPM curve of
     # the files whose beat stages ran.
     from bpm_analysis_amd.shard import FileResult, gather_file_results
-    rows = [FileResult(rank * F + f, raw_peaks=gpu_host[f]["peaks"], flags=gpu_host[f]["flags"]) for f in range(F)]
+    rows = [FileResult(seed0 + f, raw_peaks=gpu_host[f]["peaks"], flags=gpu_host[f]["flags"]) for f in range(F)]
     host_beats = None
     if args.host_beat_files > 0:
         from bpm_analysis_amd import beats
@@ -781,7 +803,7 @@ def main(args):
         ndt = time.perf_counter() - th0
         for f, a in enumerate(fast):
             if "error" not in a:
-                rows[f] = FileResult(rank * F + f, gpu_host[f]["peaks"], a["final_peaks"], a["bpm_times"], a["bpm"],
+                rows[f] = FileResult(seed0 + f, gpu_host[f]["peaks"], a["final_peaks"], a["bpm_times"], a["bpm"],
                                      gpu_host[f]["flags"])
         # the Python stages (beats.py: also HRV, slopes, debug strings) on a sample, one core
         res = gpu_host[:args.host_beat_files]
@@ -798,7 +820,7 @@ def main(args):
                                  "final_beats": int(sum(len(r["final_peaks"]) for r in done if "error" not in r))},
                       "native_equals_python": bool(same)}
     tg0 = time.perf_counter()
-    allres = gather_file_results(rows, world * F, device=cdev if world > 1 else None)
+    allres = gather_file_results(rows, total_files, device=cdev if world > 1 else None)
     gathered = None
     if rank == 0:
         got = [r for r in allres if r is not None]
@@ -818,9 +840,14 @@ def main(args):
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        value = world * F * n / (elapsed / args.steps)
-        workload = (f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
-                    f"(filter+envelope+noise floor+raw peaks)")
+        value = total_files * n / (elapsed / args.steps)
+        strong = args.files_total > 0
+        if strong:
+            workload = (f"{total_files} x {args.secs:g} s {fs} Hz mono int16 recordings in the job over {world} "
+                        f"GPU(s), {args.mode} mode (filter+envelope+noise floor+raw peaks)")
+        else:
+            workload = (f"{F} x {args.secs:g} s {fs} Hz mono int16 recordings per GPU, {args.mode} mode "
+                        f"(filter+envelope+noise floor+raw peaks)")
         # dominant kernel = the largest share of the step (summed over its launches,
         # from the warmup pass); its roofline point is per step: algorithmic bytes of
         # all its launches in a step / its time per step, the HIP-event total over
@@ -852,13 +879,14 @@ def main(args):
                     "frac_of_peak": round(step_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
         if world == 1 and not args.no_cpu and args.cpu_files != 0:
             nfc = args.cpu_files if args.cpu_files > 0 else F
-            cpu, parity = cpu_baseline(args.mode, fs, n, shard_seed0(rank, F), nfc, params, gpu_host)
+            cpu, parity = cpu_baseline(args.mode, fs, n, seed0, nfc, params, gpu_host)
         line = {
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None, "dtype": "f64",
             "data": "cpu-stub (tests only; not a measurement)" if args.cpu_stub else "synthetic",
-            "config": {"workload": workload,
+            "config": {"workload": workload, "files_total": total_files,
                        "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
                        "parallelism": f"file-sharded x{world}"},
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,

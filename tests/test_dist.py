@@ -191,7 +191,7 @@ def _bench_json(stdout: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("workload", ["metric", "c5"])
+@pytest.mark.parametrize("workload", ["metric", "strong", "c5"])
 def test_bench_launches_n_ranks(workload):
     """`python bench.py --gpus 2` starts two ranks itself (torch.distributed.run
     child, gloo under --cpu-stub), reports n_gpus 2 and gathers both ranks'
@@ -203,8 +203,10 @@ def test_bench_launches_n_ranks(workload):
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--cpu-stub", "--steps", "1", "--warmup", "1"]
     if workload == "metric":
         cmd += ["--files", "3", "--secs", "6", "--parity-files", "2", "--host-beat-files", "1"]
+    elif workload == "strong":   # BASELINE C4's shape (--files-total over the ranks), 5 recordings in the job
+        cmd += ["--files-total", "5", "--secs", "6", "--parity-files", "3", "--host-beat-files", "1"]
     else:   # 5 recordings of 10-30 min at 96 kHz stereo are too much oracle work: shrink via the chunk budget only
-        cmd += ["--workload", "c5", "--c5-files", "2", "--c5-parity-files", "1", "--c5-chunk-gb", "0.001"]
+        cmd += ["--workload", "c5", "--c5-files", "2", "--c5-chunk-gb", "0.001"]     # parity: every recording
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=repo)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _bench_json(r.stdout)
@@ -214,8 +216,16 @@ def test_bench_launches_n_ranks(workload):
         assert line["result_gather"]["files"] == 6 and line["result_gather"]["ranks_seen"] == [0, 1]
         assert line["cpu_baseline"]["per_rank"] and line["cpu_baseline"]["rank"] == 0
         assert line["parity"]["files"] == 4
+    elif workload == "strong":
+        # ranks hold recordings 0-1 and 2-4; every one checked and gathered once
+        assert line["scaling"] == "strong" and line["config"]["files_total"] == 5
+        assert line["config"]["files_per_gpu"] == 2
+        assert line["result_gather"]["files"] == 5 and line["result_gather"]["ranks_seen"] == [0, 1]
+        assert line["parity"]["files"] == 5
+        assert abs(line["value"] - 5 * 6 * 44100 / (line["ms_per_step"] / 1e3)) <= 1e-6 * line["value"]
     else:
         assert line["result_gather"]["files"] == 2 and line["scaling"] == "strong"
+        assert line["parity"]["files"] == 2
 
 
 def test_bench_refuses_world_mismatch():

@@ -1026,9 +1026,9 @@ def test_dropin_two_threads_at_once(det, tmp_path):
 def test_config_c5_shard_of_eight(det):
     """BASELINE config C5 at its stated recording shape: a shard of 8 ragged
     U[10, 30] min 96 kHz stereo int16 recordings (bench.c5_lengths, the
-    bench's own seeds) in one device batch, longest first, native mode; the
-    four shortest checked against the oracle (indices exact, envelope and
-    floor within 1e-9 of scale) and every recording's peaks sane."""
+    bench's own seeds) in one device batch, longest first, native mode; every
+    recording checked against the oracle (indices and flags exact, envelope
+    and floor within 1e-9 of scale; ~30 s of oracle time on 8 threads)."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
     import bench
@@ -1044,8 +1044,8 @@ def test_config_c5_shard_of_eight(det):
     torch.cuda.synchronize()
     host = res.to_host()
     del pcm
-    check = list(range(len(lens)))[-4:]                  # the four shortest
-    with ThreadPoolExecutor(4) as ex:
+    check = list(range(len(lens)))
+    with ThreadPoolExecutor(8) as ex:
         outs = list(ex.map(lambda k: O.detect(O.synth(seeds[k], int(lens[k]), fs, ch), fs, params, mode="native"),
                            check))
     for k, o in zip(check, outs):
