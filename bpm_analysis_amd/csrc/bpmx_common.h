@@ -130,6 +130,46 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+__device__ __forceinline__ int wave_min_i(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+/* position of the nth (0-based) set bit of x (nth < popcount(x)) */
+__device__ __forceinline__ int select64(uint64_t x, int nth) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        const int c = __popcll(x & ((1ull << w) - 1ull));
+        if (nth >= c) {
+            nth -= c;
+            x >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+/* 64 x 64 bit-matrix transpose across a wave: on entry lane e holds row e
+ * (bit j = column j), on exit lane j holds column j (bit e = row e).  Six
+ * butterfly stages, partner lane ^ s, exchanging s-bit groups.  Every lane
+ * of the wave must be active. */
+__device__ __forceinline__ uint64_t transpose64(uint64_t x) {
+    const int lane = threadIdx.x & 63;
+    uint64_t msk = 0x00000000FFFFFFFFull;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        const uint64_t p = (uint64_t)__shfl_xor((long long)x, s);
+        if (!(lane & s)) x ^= (((x >> s) ^ p) & msk) << s;
+        else x ^= ((p >> s) ^ x) & msk;
+        msk ^= msk << (s >> 1);
+    }
+    return x;
+}
 
 /* wave64 inclusive scan (sum, or running max) in registers with DPP: row
  * shifts 1/2/4/8 scan each 16-lane row, row_bcast:15 / row_bcast:31 carry the
@@ -151,6 +191,10 @@ __device__ __forceinline__ int wave_iscan_dpp(int x) {
     BPMX_DPP_STEP(0x143, 0xc)   /* row_bcast:31 -> rows 2, 3 */
 #undef BPMX_DPP_STEP
     return x;
+}
+/* wave-wide maximum (every lane active) */
+__device__ __forceinline__ int wave_max_dpp(int x) {
+    return __builtin_amdgcn_readlane(wave_iscan_dpp<true>(x), 63);
 }
 /* value of the lane below (lane 0 gets `edge`) */
 __device__ __forceinline__ int wave_shr1_dpp(int x, int edge) {

@@ -321,6 +321,13 @@ constexpr int WM_ITEMS = 18;                 /* 16-bit positions; LDS ~156 KB at
 constexpr int WM_MMAX = WM_T * WM_ITEMS;     /* 18432 decimated samples (61 s at 302 Hz) */
 constexpr int WM_TRMAX = 512;                /* troughs staged in LDS for the in-kernel interpolation */
 constexpr int WM_PMAX = 12288;               /* kept samples of the pruned variant */
+/* per-wave output-block scratch of k_rollq_wm_t (32-bit words): collected
+ * members (16 lanes need at most 15 + 30 + 30 + 2: k spread + low-count
+ * spread + excluded members + two; a block of 64 that needs more than fits
+ * runs as four passes of 16), then as many partial-member records.  Small,
+ * so that the sorted values fit beside it up to ~8000 kept samples. */
+constexpr int WM_DCAP = 96;
+constexpr int WM_WSCR = 2 * WM_DCAP;
 /* dynamic LDS of k_rollq_wm_t: trough tables | (pruned) kept masks, prefix,
  * bins | (pruned) kept positions | phase area (histogram / sort / matrix) */
 struct WmLayout {
@@ -340,7 +347,8 @@ __host__ __device__ inline WmLayout wm_layout(int64_t nmax, bool prune) {
     const int64_t m8 = (m + 7) & ~7LL;
     const int64_t NBK = WM_MMAX / 64 + 2;                              /* per-64 tables */
     const int64_t sort_b = 8 * m8 + (int64_t)(WM_T / 64) * 128 * 4;   /* pos x2, key halves, counters */
-    const int64_t wm_b = 4 * m8 + L * (2 * NW + 1) * 8;               /* sequences x2, levels */
+    const int64_t wm_b = ((4 * m8 + 15) & ~15LL) + (int64_t)(WM_T / 64) * WM_WSCR * 4;   /* index arrays, block scratch */
+    (void)L; (void)NW;
     const int64_t hist_b = prune ? NBK * 64 * 2 + (int64_t)(WM_T / 64) * 64 * 4 + n : 0;   /* + bin per sample */
     int64_t area = sort_b > wm_b ? sort_b : wm_b;
     area = area > hist_b ? area : hist_b;

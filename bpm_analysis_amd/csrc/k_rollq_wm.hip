@@ -32,13 +32,15 @@
  *      wave-contiguous, so a stable rank is: per-wave digit counter (LDS
  *      atomic, issued in slot order) + peers below in the same round (ballot
  *      match) + one (digit, wave) block scan.
- *   2. wavelet matrix over the rank sequence (ceil(log2 m) levels): per level
- *      a bit vector with a rank directory, {word, ones-before} per 32 samples.
- *   3. every output independently: its window's k-th smallest by one top-down
- *      descent, the (k+1)-th by walking up the rank order to the next rank
- *      inside the window; pandas' linear interpolation, nobs / min_periods
- *      from the window bounds.  NaN outputs are a prefix and a suffix (nobs is
- *      unimodal), filled from the first and last valid output.
+ *   2. outputs, 64 consecutive ones per wave step: a rank cursor moved from
+ *      block to block, the block's candidate ranks collected from it, and each
+ *      lane's k-th / (k+1)-th smallest selected from a transposed 64 x 64
+ *      membership bit matrix (details at the phase).  pandas' linear
+ *      interpolation, nobs / min_periods from the window bounds.  NaN outputs
+ *      are a prefix and a suffix (nobs is unimodal), filled from the first and
+ *      last valid output.  (r01-r03 answered every output by a top-down descent
+ *      of a wavelet matrix over the rank sequence; building its levels and the
+ *      descents cost more than the whole of this phase.)
  * Recordings longer than WM_MMAX decimated samples take k_rolling_quantile.
  */
 #include "bpmx_common.h"
@@ -65,12 +67,6 @@ __device__ __forceinline__ uint64_t match8(uint32_t dg) {
     }
     return m;
 }
-
-/* rank directory entry: 32 positions' bits and the ones before them */
-struct WmRec {
-    uint32_t word;
-    uint32_t ones;
-};
 
 template <bool PRUNE>
 __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full) {
@@ -131,14 +127,13 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         return;
     }
     extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_first, s_last, s_Z[16], s_wt[NWV], s_mk;
+    __shared__ int s_first, s_last, s_wt[NWV], s_mk;
     __shared__ unsigned long long s_or[NWV], s_and[NWV];
     __shared__ double s_vmin, s_vmax;
 
     const double *dense = A.dense + d0;
     double *out = A.out + d0;
-    /* kept index of each rank */
-    uint16_t *ps = chunked ? A.wm_pos_ch + ((int64_t)f * gridDim.y + blockIdx.y) * WM_PMAX : pos_scratch + d0;
+    (void)pos_scratch;
     if (!chunked) t0 = A.troughs[d0];
     const int mall = (int)(top - t0);                        /* finite samples dense[t0:top) */
     const WmLayout Lay = wm_layout(chunked ? top - t0 : n, PRUNE);
@@ -442,6 +437,9 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         return lpre[p >> 6] + __popcll(mk & ((1ull << (p & 63)) - 1ull));
     };
     STAMP(7);
+#ifdef RQ_DIAG_M
+    if (threadIdx.x == 0) _st_acc[13] = (unsigned long long)m;   /* diagnostics: kept samples */
+#endif
 
     /* LDS, sort phase: posA[m8] | posB[m8] | kh[m8] | cnt[NWV][128] (two 16-bit counters per word).
      * Slots >= m are padding: they sort last, so they are neither stored nor counted. */
@@ -453,246 +451,364 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
     uint32_t *kh = (uint32_t *)(posB + m8);
     uint32_t *cnt = kh + m8;
 
-    /* ---------------- 1. ranks by LSD radix sort ---------------- */
-    uint64_t kor = 0, kand = ~0ull;
-    for (int p = tid; p < m; p += WM_T) {
-        posA[p] = (uint16_t)p;                               /* slot order == index order */
-        const uint64_t k = wm_key(dval(t0 + spos(p)));
-        kh[p] = (uint32_t)k;
-        kor |= k;
-        kand &= k;
+    /* ---------------- 1. ranks by LSD radix sort ----------------
+     * Keys: the order-preserving 64-bit key minus the curve's lowest key,
+     * shifted right so that it spans at most 40 bits (five 8-bit digits
+     * instead of the seven a span of a few octaves takes).  Distinct values
+     * closer than the shift could share a compact key and keep index order;
+     * the sorted values are checked afterwards and any descent hands the
+     * recording to the unpruned variant (full-width keys), as too many kept
+     * samples do. */
+    const size_t wsc = ((size_t)4 * m8 + 15) & ~(size_t)15;
+    const size_t svl_off = wsc + (size_t)NWV * WM_WSCR * 4;
+    double *svl = svl_off + (size_t)8 * m <= Lay.total - Lay.area ? (double *)(smem + Lay.area + svl_off) : nullptr;
+    uint64_t kbase = 0;
+    int shc = 0;
+    if (PRUNE && svl) {
+        /* the curve lies between its lowest and highest trough up to rounding;
+         * a sample past them clamps to the ends (and the check catches it) */
+        kbase = wm_key(s_vmin);
+        const uint64_t ktop = wm_key(s_vmax);
+        const int nbits = ktop > kbase ? 64 - __clzll((long long)(ktop - kbase)) : 0;
+        shc = nbits > 40 ? nbits - 40 : 0;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        kor |= (uint64_t)__shfl_xor((long long)kor, o);
-        kand &= (uint64_t)__shfl_xor((long long)kand, o);
-    }
-    if (lane == 0) { s_or[wid] = kor; s_and[wid] = kand; }
-    __syncthreads();
-    uint64_t vary = 0;
     {
-        uint64_t o = 0, a = ~0ull;
-        for (int w = 0; w < NWV; ++w) { o |= s_or[w]; a &= s_and[w]; }
-        vary = o ^ a;                                        /* key bits that differ somewhere */
-    }
-    STAMP(0);
-    uint32_t *wc = cnt + wid * 128;
-    for (int d = 0; d < 8; ++d) {
-        if (d == 4 && (vary >> 32)) {                        /* high halves, indexed by index */
-            for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(wm_key(dval(t0 + spos(p))) >> 32);
-            __syncthreads();
+        auto ckey = [&](int p) -> uint64_t {
+            const uint64_t k = wm_key(dval(t0 + spos(p)));
+            return shc ? (k > kbase ? k - kbase : 0ull) >> shc : k;
+        };
+        uint64_t kor = 0, kand = ~0ull;
+        for (int p = tid; p < m; p += WM_T) {
+            posA[p] = (uint16_t)p;                           /* slot order == index order */
+            const uint64_t k = ckey(p);
+            kh[p] = (uint32_t)k;
+            kor |= k;
+            kand &= k;
         }
-        if (((vary >> (8 * d)) & 0xFFull) == 0) continue;    /* uniform: constant digit, order unchanged */
-        const int sh = 8 * (d & 3);
-        for (int j = lane; j < 128; j += 64) wc[j] = 0;
-        /* digits of all this lane's items first (independent LDS reads) */
-        uint32_t dg8[(MAXIT + 3) / 4], rk16[(MAXIT + 1) / 2];   /* packed: digit 8 b, rank 16 b */
-#pragma unroll
-        for (int i = 0; i < MAXIT; ++i) {
-            const int slot = wid * S + i * 64 + lane;
-            const uint32_t dg = (i < IT && slot < m) ? (kh[posA[slot]] >> sh) & 0xFFu : 0u;
-            if ((i & 3) == 0) dg8[i >> 2] = dg; else dg8[i >> 2] |= dg << (8 * (i & 3));
+        for (int o = 32; o > 0; o >>= 1) {
+            kor |= (uint64_t)__shfl_xor((long long)kor, o);
+            kand &= (uint64_t)__shfl_xor((long long)kand, o);
         }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int i = 0; i < MAXIT; ++i) {
-            if (i < IT) {
-                const int slot = wid * S + i * 64 + lane;
-                const bool valid = slot < m;
-                const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                const uint64_t peers = match8(dg) & __ballot(valid);
-                const uint64_t below = peers & lanemask_lt();
-                const int leader = valid ? __ffsll((long long)peers) - 1 : lane;
-                uint32_t base = 0;
-                if (valid && below == 0)   /* LDS atomics of one wave land in issue (= slot) order */
-                    base = atomicAdd(&wc[dg >> 1], (uint32_t)__popcll(peers) << (16 * (dg & 1)));
-                base = (uint32_t)__shfl((int)base, leader);
-                const uint32_t rnk = ((base >> (16 * (dg & 1))) & 0xFFFFu) + (uint32_t)__popcll(below);
-                if ((i & 1) == 0) rk16[i >> 1] = rnk; else rk16[i >> 1] |= rnk << 16;
-            }
-        }
+        if (lane == 0) { s_or[wid] = kor; s_and[wid] = kand; }
         __syncthreads();
-        STAMP(1);
-        /* exclusive scan over (digit, wave) order, 4 consecutive entries per thread */
+        uint64_t vary = 0;
         {
-            uint32_t v[4], s = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = tid * 4 + u, dg = e / NWV, w = e % NWV;
-                v[u] = (cnt[w * 128 + (dg >> 1)] >> (16 * (dg & 1))) & 0xFFFFu;
-                s += v[u];
+            uint64_t o = 0, a = ~0ull;
+            for (int w = 0; w < NWV; ++w) { o |= s_or[w]; a &= s_and[w]; }
+            vary = o ^ a;                                    /* key bits that differ somewhere */
+        }
+        STAMP(0);
+        uint32_t *wc = cnt + wid * 128;
+        for (int d = 0; d < 8; ++d) {
+            if (d == 4 && (vary >> 32)) {                    /* high halves, indexed by index */
+                for (int p = tid; p < m; p += WM_T) kh[p] = (uint32_t)(ckey(p) >> 32);
+                __syncthreads();
             }
-            uint32_t x = s;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o) x += y;
+            if (((vary >> (8 * d)) & 0xFFull) == 0) continue;   /* uniform: constant digit, order unchanged */
+            const int sh = 8 * (d & 3);
+            for (int j = lane; j < 128; j += 64) wc[j] = 0;
+            /* digits of all this lane's items first (independent LDS reads) */
+            uint32_t dg8[(MAXIT + 3) / 4], rk16[(MAXIT + 1) / 2];   /* packed: digit 8 b, rank 16 b */
+#pragma unroll
+            for (int i = 0; i < MAXIT; ++i) {
+                const int slot = wid * S + i * 64 + lane;
+                const uint32_t dg = (i < IT && slot < m) ? (kh[posA[slot]] >> sh) & 0xFFu : 0u;
+                if ((i & 3) == 0) dg8[i >> 2] = dg; else dg8[i >> 2] |= dg << (8 * (i & 3));
             }
-            if (lane == 63) s_wt[wid] = (int)x;
-            __syncthreads();
-            uint32_t run = x - s;
-            for (int w = 0; w < wid; ++w) run += (uint32_t)s_wt[w];
-            /* the two halves of a counter word are different threads' entries:
-             * write 16-bit halves */
-            uint16_t *c16 = (uint16_t *)cnt;
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = tid * 4 + u, dg = e / NWV, w = e % NWV;
-                c16[(w * 128 + (dg >> 1)) * 2 + (dg & 1)] = (uint16_t)run;
-                run += v[u];
-            }
-        }
-        __syncthreads();
-        STAMP(2);
-        const uint16_t *c16 = (const uint16_t *)cnt;
-#pragma unroll
-        for (int i = 0; i < MAXIT; ++i) {
-            const int slot = wid * S + i * 64 + lane;
-            if (i < IT && slot < m) {
-                const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                const uint32_t rnk = (rk16[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                posB[(int)c16[(wid * 128 + (dg >> 1)) * 2 + (dg & 1)] + (int)rnk] = posA[slot];
-            }
-        }
-        __syncthreads();
-        uint16_t *t = posA; posA = posB; posB = t;
-        STAMP(3);
-    }
-    /* posA[r] = index of rank r.  Build: seqA = the free pos buffer,
-     * seqB = posA once consumed; levels over the dead kh / cnt. */
-    const int L = m > 1 ? 32 - __clz(m - 1) : 1;              /* levels: ranks < 2^L */
-    const int NW = (m + 63) >> 6;                             /* 64-bit words per level */
-    const int NR = 2 * NW + 1;                                /* 32-bit records per level (+ sentinel) */
-    uint16_t *seqA = posB, *seqB = posA;
-    WmRec *lv = (WmRec *)kh;                                  /* [L][NR] */
-    for (int r = tid; r < m; r += WM_T) {
-        const int p = posA[r];
-        ps[r] = (uint16_t)p;
-        seqA[p] = (uint16_t)r;
-    }
-    __syncthreads();
-    STAMP(4);
-
-    /* ---------------- 2. wavelet matrix ---------------- */
-    constexpr int CWMAX = (MMAX / 64 + NWV - 1) / NWV;       /* words per wave at the maximum */
-    const int cw = (NW + NWV - 1) / NWV;                     /* words per wave (<= CWMAX) */
-    const int wb = wid * cw, nwv = max(0, min(NW, wb + cw) - wb);
-    for (int l = L - 1; l >= 0; --l) {
-        WmRec *row = lv + l * NR;
-        /* this wave's words into registers first (independent LDS reads), then
-         * ones among them (ballots are wave-uniform: scalar sums) */
-        uint32_t sq[CWMAX];
-        uint32_t wones = 0;
-#pragma unroll
-        for (int w = 0; w < CWMAX; ++w) {
-            const int p = (wb + w) * 64 + lane;
-            sq[w] = (w < nwv && p < m) ? (uint32_t)seqA[p] : 0xFFFFFFFFu;   /* all-ones: invalid */
-        }
-#pragma unroll
-        for (int w = 0; w < CWMAX; ++w)
-            wones += (uint32_t)__popcll(__ballot(sq[w] != 0xFFFFFFFFu && ((sq[w] >> l) & 1)));
-        if (lane == 0) s_wt[wid] = (int)wones;
-        __syncthreads();
-        uint32_t run = 0, tot = 0;
-        for (int w = 0; w < NWV; ++w) {
-            const uint32_t t = (uint32_t)s_wt[w];
-            run += w < wid ? t : 0u;
-            tot += t;
-        }
-        const int Z = m - (int)tot;                          /* zeros of this level */
-        if (tid == 0) {
-            row[2 * NW] = WmRec{0u, tot};
-            s_Z[l] = Z;
-        }
-        /* stable partition (zeros, then ones) and the rank directory */
-#pragma unroll
-        for (int w = 0; w < CWMAX; ++w) {
-            if (w < nwv) {
-                const int p = (wb + w) * 64 + lane;
-                const bool bit = sq[w] != 0xFFFFFFFFu && ((sq[w] >> l) & 1);
-                const uint64_t word = __ballot(bit);
-                if (lane == 0) {
-                    row[2 * (wb + w)] = WmRec{(uint32_t)word, run};
-                    row[2 * (wb + w) + 1] = WmRec{(uint32_t)(word >> 32), run + (uint32_t)__popc((uint32_t)word)};
+            for (int i = 0; i < MAXIT; ++i) {
+                if (i < IT) {
+                    const int slot = wid * S + i * 64 + lane;
+                    const bool valid = slot < m;
+                    const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                    const uint64_t peers = match8(dg) & __ballot(valid);
+                    const uint64_t below = peers & lanemask_lt();
+                    const int leader = valid ? __ffsll((long long)peers) - 1 : lane;
+                    uint32_t base = 0;
+                    if (valid && below == 0)   /* LDS atomics of one wave land in issue (= slot) order */
+                        base = atomicAdd(&wc[dg >> 1], (uint32_t)__popcll(peers) << (16 * (dg & 1)));
+                    base = (uint32_t)__shfl((int)base, leader);
+                    const uint32_t rnk = ((base >> (16 * (dg & 1))) & 0xFFFFu) + (uint32_t)__popcll(below);
+                    if ((i & 1) == 0) rk16[i >> 1] = rnk; else rk16[i >> 1] |= rnk << 16;
                 }
-                const int o1 = (int)run + __popcll(word & lanemask_lt());
-                if (sq[w] != 0xFFFFFFFFu) seqB[bit ? Z + o1 : p - o1] = (uint16_t)sq[w];
-                run += (uint32_t)__popcll(word);
             }
+            __syncthreads();
+            STAMP(1);
+            /* exclusive scan over (digit, wave) order, 4 consecutive entries per thread */
+            {
+                uint32_t v[4], sm = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e = tid * 4 + u, dg = e / NWV, w = e % NWV;
+                    v[u] = (cnt[w * 128 + (dg >> 1)] >> (16 * (dg & 1))) & 0xFFFFu;
+                    sm += v[u];
+                }
+                uint32_t x = sm;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o);
+                    if (lane >= o) x += y;
+                }
+                if (lane == 63) s_wt[wid] = (int)x;
+                __syncthreads();
+                uint32_t run = x - sm;
+                for (int w = 0; w < wid; ++w) run += (uint32_t)s_wt[w];
+                /* the two halves of a counter word are different threads' entries:
+                 * write 16-bit halves */
+                uint16_t *c16 = (uint16_t *)cnt;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e = tid * 4 + u, dg = e / NWV, w = e % NWV;
+                    c16[(w * 128 + (dg >> 1)) * 2 + (dg & 1)] = (uint16_t)run;
+                    run += v[u];
+                }
+            }
+            __syncthreads();
+            STAMP(2);
+            const uint16_t *c16 = (const uint16_t *)cnt;
+#pragma unroll
+            for (int i = 0; i < MAXIT; ++i) {
+                const int slot = wid * S + i * 64 + lane;
+                if (i < IT && slot < m) {
+                    const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                    const uint32_t rnk = (rk16[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                    posB[(int)c16[(wid * 128 + (dg >> 1)) * 2 + (dg & 1)] + (int)rnk] = posA[slot];
+                }
+            }
+            __syncthreads();
+            uint16_t *t = posA; posA = posB; posB = t;
+            STAMP(3);
         }
-        __syncthreads();
-        uint16_t *t = seqA; seqA = seqB; seqB = t;
     }
-    /* rank -> index back into LDS over the dead sequence buffer */
-    __threadfence_block();
-    uint16_t *posR = seqA;
-    for (int r = tid; r < m; r += WM_T) posR[r] = ps[r];
-    /* sorted values in LDS past the levels when they fit (pruned variant);
-     * otherwise each output evaluates its two values from the troughs */
-    double *svl = nullptr;
-    if (PRUNE) {
-        const size_t off = ((size_t)4 * m8 + (size_t)L * NR * 8 + 15) & ~(size_t)15;
-        if (off + (size_t)8 * m <= Lay.total - Lay.area) svl = (double *)(smem + Lay.area + off);
-    }
-    __syncthreads();
-    if (svl) {
+    /* posA[r] = structure index of rank r; posB becomes its inverse */
+    uint16_t *posR = posA, *rkx = posB;
+    for (int r = tid; r < m; r += WM_T) rkx[posR[r]] = (uint16_t)r;
+    if (svl)
         for (int r = tid; r < m; r += WM_T) svl[r] = dval(t0 + spos(posR[r]));
-        __syncthreads();
+    __syncthreads();
+    if (shc) {
+        bool down = false;                                   /* a compact key hid an order */
+        for (int r = tid; r + 1 < m; r += WM_T) down |= svl[r] > svl[r + 1];
+        if (__syncthreads_or(down)) {                        /* the full-width variant redoes it */
+            if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
+            return;
+        }
     }
+    /* per-wave block scratch past the two index arrays: the collected ranks,
+     * then the partial members; the sorted values past that when they fit
+     * (else each output evaluates its two) */
+    uint32_t *wl = (uint32_t *)(smem + Lay.area + wsc) + (size_t)wid * WM_WSCR;
     STAMP(5);
 
-    /* ---------------- 3. outputs ---------------- */
-    auto rk = [&](const WmRec *row, int i) {
-        const WmRec r = row[i >> 5];
-        return (int)r.ones + __popc(r.word & ((1u << (i & 31)) - 1u));
-    };
-    /* the k-th smallest of structure indices [lo, hi): one top-down descent */
-    auto kth = [&](int lo, int hi, int k) {
-        int r = 0;
-        for (int l = L - 1; l >= 0; --l) {
-            const WmRec *row = lv + l * NR;
-            const int o0 = rk(row, lo), o1 = rk(row, hi);
-            const int z = (hi - o1) - (lo - o0);
-            if (k < z) { lo -= o0; hi -= o1; }
-            else { k -= z; const int Z = s_Z[l]; lo = Z + o0; hi = Z + o1; r |= 1 << l; }
+    /* ---------------- 2. outputs, a block of 64 at a time per wave ----------------
+     * Lane j of a wave takes output i = i0 + j.  Its window's kept samples are
+     * the structure indices [plo_j, phi_j); plo and phi do not decrease with j,
+     * and within a block each moves by at most 63 (the window moves by one
+     * position per output).  U = [plo_first, phi_last) over the block's valid
+     * lanes.  Lane j's k-th smallest kept sample is its own t_j-th member in
+     * rank order (t_j = k_j - low samples in its window).  A rank cursor rs is
+     * kept as U's Tmin-th member (Tmin = min_j t_j), moved from the previous
+     * block's (U shifts by at most 64 indices at each end: one ballot per end
+     * corrects the count of members below rs; the cursor then walks 64 ranks
+     * per step).  From rs the next `need` members of U are collected in rank
+     * order.  Lane j has Tmin - (its excluded members below rs) own members
+     * before rs, so its k-th and (k+1)-th smallest are its na-th and nb-th own
+     * member among the collected ones; `need` bounds how far that can lie,
+     * excluded members included.  A collected member at position p belongs to
+     * the lanes j with s_j <= p < e_j, i.e. the lane range [p - i0 - off,
+     * p - i0 - off + W) (the window bounds' clamps never bind at a kept
+     * position); the few members that miss some valid lane ("partial": within
+     * 63 positions of U's ends) are listed, and each lane skips the ones it
+     * misses while counting to na and nb.  Every step is a wave-wide operation;
+     * no workgroup barrier. */
+    auto target = [&](int nb, double &idxf, bool &interp) -> int {
+        idxf = 0;
+        int k = 0;
+        if (nb > 1) {
+            idxf = q * (double)(nb - 1);
+            k = (int)idxf;
         }
-        return r;
+        interp = !(nb == 1 || (double)k == idxf);
+        return k;
     };
+    const uint64_t ltm = lanemask_lt();
+    const int off = (int)((W - 1) / 2), Wi = (int)W, ni = (int)n, t0i = (int)t0;
     int vfirst = INT_MAX, vlast = -1;
-    for (int64_t i = o0 + tid; i < o1; i += WM_T) {
-        int64_t s, e;
-        win_bounds(i, n, W, s, e);
-        const int64_t lo = s > t0 ? s : t0;
-        const int64_t nobs = e > lo ? e - lo : 0;
-        double res = __builtin_nan("");
-        if (nobs >= minp && nobs > 0) {
-            const int plo = kidx((int)(lo - t0)), phi = kidx((int)(e - t0));
-            double idxf = 0;
-            int64_t k = 0;
-            if (nobs > 1) {
-                idxf = q * (double)(nobs - 1);
-                k = (int64_t)idxf;
-            }
-            const bool interp = !(nobs == 1 || (double)k == idxf);
-            /* the window's samples below the structure rank before every kept one */
-            const int ra = kth(plo, phi, (int)k - (PRUNE ? lidx((int)(e - t0)) - lidx((int)(lo - t0)) : 0));
-            const double va = svl ? svl[ra] : dval(t0 + spos(posR[ra]));
-            if (!interp) {
-                res = va;
-            } else {
-                /* k + 1 < (kept samples in the window) here, so an in-window
-                 * rank above ra exists: the successor in the window */
-                int rb = ra + 1, pb;
-                for (;;) {
-                    pb = posR[rb];
-                    if (pb >= plo && pb < phi) break;
-                    ++rb;
+    uint32_t *wpart = wl + WM_DCAP;                          /* partial members: L index | lane range */
+    {
+        const int NBLK = (int)((o1 - o0 + 63) >> 6);
+        const int NBW = (NBLK + NWV - 1) / NWV;
+        const int b0 = wid * NBW, b1 = min(NBLK, b0 + NBW);
+        int rs = 0, cU = 0, pPlo = -1, pPhi = -1;            /* wave-uniform cursor */
+        for (int bk = b0; bk < b1; ++bk) {
+            const int i0 = (int)o0 + (bk << 6), i = i0 + lane;
+            bool valid = false;
+            int plo = 0, phi = 0, t = 0, nobs = 0;
+            if (i < (int)o1) {
+                const int ee = i + 1 + off, ss = ee - Wi;
+                const int e = ee < ni ? ee : ni, sc = ss > 0 ? ss : 0;
+                const int lo = sc > t0i ? sc : t0i;
+                nobs = e > lo ? e - lo : 0;
+                if (nobs >= minp && nobs > 0) {
+                    valid = true;
+                    plo = kidx(lo - t0i);
+                    phi = kidx(e - t0i);
+                    const int lw = PRUNE ? lidx(e - t0i) - lidx(lo - t0i) : 0;
+                    double idxf;
+                    bool interp;
+                    t = target(nobs, idxf, interp) - lw;
                 }
-                const double vb = svl ? svl[rb] : dval(t0 + spos(pb));
-                res = va + (vb - va) * (idxf - (double)k);
             }
-            vfirst = vfirst < (int)i ? vfirst : (int)i;
-            vlast = vlast > (int)i ? vlast : (int)i;
+            const uint64_t vm0 = __ballot(valid);
+            if (vm0 == 0) {                                  /* NaN block: the cursor restarts after it */
+                if (i < (int)o1) out[i] = __builtin_nan("");
+                rs = cU = 0;
+                pPlo = -1;
+                continue;
+            }
+            /* a block whose members to collect exceed the scratch runs as four
+             * passes of 16 lanes (need <= 15 + 2 * 30 + 2 there; 64 lanes need
+             * about 30 on the bench's curves, at most 63 + 2 * 126 + 2) */
+            int ja = __ffsll((long long)vm0) - 1, jb = 63 - __clzll((long long)vm0);
+            int Plo = __builtin_amdgcn_readlane(plo, ja), PloMax = __builtin_amdgcn_readlane(plo, jb);
+            int PhiMin = __builtin_amdgcn_readlane(phi, ja), Phi = __builtin_amdgcn_readlane(phi, jb);
+            int Tmin = -wave_max_dpp(valid ? -t : INT_MIN + 1);
+            int need = wave_max_dpp(valid ? t - Tmin + (plo - Plo) + (Phi - phi) : 0) + 2;
+            const int npass = need > WM_DCAP ? 4 : 1;
+#ifdef BPMX_STAMPS
+            if (threadIdx.x == 0) _st_acc[12] += 1000000ull * (npass > 1) + (unsigned long long)need;   /* diagnostics: 4-pass blocks, need */
+#endif
+            const bool valid0 = valid;
+            double res = __builtin_nan("");
+            for (int pass = 0; pass < npass; ++pass) {
+                if (npass > 1) {
+                    valid = valid0 && (lane >> 4) == pass;
+                    const uint64_t vm = __ballot(valid);
+                    if (vm == 0) continue;
+                    ja = __ffsll((long long)vm) - 1;
+                    jb = 63 - __clzll((long long)vm);
+                    Plo = __builtin_amdgcn_readlane(plo, ja); PloMax = __builtin_amdgcn_readlane(plo, jb);
+                    PhiMin = __builtin_amdgcn_readlane(phi, ja); Phi = __builtin_amdgcn_readlane(phi, jb);
+                    Tmin = -wave_max_dpp(valid ? -t : INT_MIN + 1);
+                    need = min(WM_DCAP, wave_max_dpp(valid ? t - Tmin + (plo - Plo) + (Phi - phi) : 0) + 2);
+                }
+                STAMP(4);
+                /* the cursor's count for this U: members dropped on the left, added on the right */
+                if (pPlo >= 0) {
+                    const int xl = pPlo + lane, xe = pPhi + lane;
+                    const bool bl = xl < Plo && (int)rkx[xl] < rs;
+                    const bool be = xe < Phi && (int)rkx[xe] < rs;
+                    cU += __popcll(__ballot(be)) - __popcll(__ballot(bl));
+                } else {
+                    rs = cU = 0;
+                }
+                /* move rs to U's Tmin-th member */
+                for (int guard = 0; guard <= m / 64 + 2; ++guard) {
+                    if (cU <= Tmin) {
+                        const int rr = rs + lane;
+                        const int x = rr < m ? (int)posR[rr] : -1;
+                        const uint64_t bm = __ballot(x >= Plo && x < Phi);
+                        const int c = __popcll(bm);
+                        if (cU + c <= Tmin) {
+                            rs += 64;
+                            cU += c;
+                            continue;
+                        }
+                        rs += select64(bm, Tmin - cU);
+                    } else {
+                        const int st = rs > 64 ? rs - 64 : 0, rr = st + lane;
+                        const int x = rr < rs ? (int)posR[rr] : -1;
+                        const uint64_t bm = __ballot(x >= Plo && x < Phi);
+                        const int c = __popcll(bm);
+                        if (cU - c > Tmin) {
+                            rs = st;
+                            cU -= c;
+                            continue;
+                        }
+                        rs = st + select64(bm, Tmin - (cU - c));
+                    }
+                    cU = Tmin;
+                    break;
+                }
+                /* own members below rs: Tmin minus this lane's excluded ones there */
+                int na;
+                {
+                    const int xL = Plo + lane, xR = PhiMin + lane;
+                    const uint64_t mL = __ballot(xL < PloMax && (int)rkx[xL] < rs);
+                    const uint64_t mR = __ballot(xR < Phi && (int)rkx[xR] < rs);
+                    const int dl = valid ? plo - Plo : 0, dr = valid ? phi - PhiMin : 0;   /* both <= 63 */
+                    na = t - Tmin + __popcll(mL & ((1ull << dl) - 1ull)) + __popcll(mR >> dr);
+                }
+                STAMP(14);
+                /* the next `need` members of U from rs, in rank order; partial ones listed */
+                int cnt = 0, np = 0;
+                const int lbase = i0 + off;                      /* member at position p: lanes [p - lbase, p - lbase + W) */
+                for (int r = rs; cnt < need && r < m; r += 64) {
+                    const int rr = r + lane;
+                    const int x = rr < m ? (int)posR[rr] : -1;
+                    const bool mb = x >= Plo && x < Phi;
+                    const uint64_t bm = __ballot(mb);
+                    const int slot = cnt + __popcll(bm & ltm);
+                    bool part = false;
+                    uint32_t lr = 0;
+                    if (mb && slot < need) {
+                        wl[slot] = (uint32_t)rr;
+                            const int pos = t0i + spos(x);
+                        const int l0 = pos - lbase, l1 = l0 + Wi - 1;
+                        const int ca = l0 > ja ? l0 : ja, cb = l1 < jb ? l1 : jb;
+                        part = ca > ja || cb < jb;
+                        /* an empty range (cb < ca) misses every lane */
+                        lr = (uint32_t)slot | ((uint32_t)(ca & 127) << 16) | ((uint32_t)((cb + 1) & 127) << 24);
+                    }
+                    const uint64_t pm = __ballot(part);
+                    if (part) wpart[np + __popcll(pm & ltm)] = lr;
+                    np += __popcll(pm);
+                    cnt += __popcll(bm);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                STAMP(15);
+                /* this lane's na-th own member and the next: skip the partial ones it
+                 * misses (usually none or one or two per block) */
+                int ia = na, ib = -1;
+                for (int u = 0; u < np; ++u) {
+                    const uint32_t pr = wpart[u];
+                    const int li = (int)(pr & 0xFFFFu), ca = (int)((pr >> 16) & 127u), cb1 = (int)(pr >> 24);
+                    const bool miss = lane < ca || lane >= cb1;
+                    if (ib < 0) {
+                        if (li <= ia) {
+                            if (miss) ++ia;
+                            continue;
+                        }
+                        ib = ia + 1;
+                    }
+                    if (li == ib && miss) ++ib;
+                }
+                if (ib < 0) ib = ia + 1;
+                ia = ia < need ? ia : need - 1;                  /* (never binds; keeps a corrupted walk in bounds) */
+                ib = ib < need ? ib : need - 1;
+                if (valid) {
+                    double idxf;
+                    bool interp;
+                    const int k = target(nobs, idxf, interp);
+                    const double va = svl ? svl[wl[ia]] : dval(t0 + spos(posR[wl[ia]]));
+                    if (!interp) {
+                        res = va;
+                    } else {
+                        const double vb = svl ? svl[wl[ib]] : dval(t0 + spos(posR[wl[ib]]));
+                        res = va + (vb - va) * (idxf - (double)k);
+                    }
+                    vfirst = vfirst < i ? vfirst : i;
+                    vlast = vlast > i ? vlast : i;
+                }
+                __builtin_amdgcn_wave_barrier();                 /* the scratch is rewritten by the next pass */
+                pPlo = Plo;
+                pPhi = Phi;
+            }
+            if (i < (int)o1) out[i] = res;
+            STAMP(6);
         }
-        out[i] = res;
     }
     for (int o = 32; o > 0; o >>= 1) {
         vfirst = min(vfirst, __shfl_xor(vfirst, o));
