@@ -184,8 +184,8 @@ def algorithmic_bytes_total(mode: str, F: int, frames: int, nd: int, channels: i
 PMC_NAMES = {"k_native_blocks": ("k_native_blocks_mfma", "k_native_blocks_dma", "k_native_blocks_i16",
                                  "k_native_blocks_gen"),
              "k_rollq_wm": ("k_rollq_wm_t",),
-             "k_find_peaks[troughs]": ("k_find_peaks_lds", "k_find_peaks"),
-             "k_find_peaks[peaks]": ("k_find_peaks_lds", "k_find_peaks")}
+             "k_find_peaks[troughs]": ("k_find_peaks[troughs]", "k_find_peaks_lds", "k_find_peaks"),
+             "k_find_peaks[peaks]": ("k_find_peaks[peaks]", "k_find_peaks_lds", "k_find_peaks")}
 
 
 def pmc_traffic(mode: str, kernel: str, workload: str, launches_per_step: float):

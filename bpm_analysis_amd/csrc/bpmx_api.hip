@@ -20,6 +20,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *ac
     for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
     if (nraw) nraw[f] = 0;                                   /* the caller's raw-trough counts */
     if (z1) z1[f] = 0;                                       /* draft exact masks (one int per recording) */
-    if (z2) { z2[2 * f] = 0; z2[2 * f + 1] = 0; }            /* draft undecided counters (two ints) */
+    if (z2) { z2[f] = 0; z2[n_files + f] = 0; }              /* draft undecided counters nund[f], nund[F + f] */
 }
 
 /* recordings with >= 5 raw troughs reach the rolling quantile: with a noise
@@ -123,11 +124,12 @@ void bpmx_destroy(bpmx_ctx *ctx) {
         if (kv.second.first) (void)hipFree(kv.second.first);
     for (auto &r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : ctx->pool) (void)hipEventDestroy(e);
-    for (int i = 0; i < bpmx_ctx::NSIDE; ++i) {
+    for (int i = 0; i < bpmx_ctx::NSIDE && !ctx->root; ++i) {   /* a pipeline sub-context borrows its root's */
         if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
         if (ctx->side_join[i]) (void)hipEventDestroy(ctx->side_join[i]);
     }
-    if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
+    if (ctx->side_fork && !ctx->root) (void)hipEventDestroy(ctx->side_fork);
+    if (ctx->stats_ev) (void)hipEventDestroy(ctx->stats_ev);
     for (bpmx_ctx *c : ctx->pipe_sub) bpmx_destroy(c);
     bpmx::longfft_free(ctx);
     if (ctx->pipe_env) (void)hipStreamDestroy(ctx->pipe_env);
@@ -242,11 +244,22 @@ int bpmx_stats(bpmx_ctx *ctx, int64_t *out, int n) {
     int64_t h[BPMX_NSTATS] = {};
     auto it = ctx->bufs.find("stats");
     if (it != ctx->bufs.end()) {
-        HIP_TRY(hipStreamSynchronize(ctx->stats_stream));
+        if (ctx->stats_ev) HIP_TRY(hipEventSynchronize(ctx->stats_ev));
         HIP_TRY(hipMemcpy(h, it->second.first, sizeof h, hipMemcpyDeviceToHost));
     }
     for (int i = 0; i < n; ++i) out[i] = i < BPMX_NSTATS ? h[i] : 0;
     return BPMX_NSTATS;
+}
+
+/* the rolling-quantile kernels' dynamic-LDS limit, raised once per process
+ * to the largest layout they take (not per launch on the run path) */
+static void wm_lds_attr() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const int mx = (int)wm_layout(WM_MMAX, false).total;
+        (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    });
 }
 
 static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream,
@@ -279,10 +292,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         int src = BPMX_OK;
         d_stats = (int64_t *)ctx->pr()->buf("stats", BPMX_NSTATS * 8, &src);
         if (src != BPMX_OK) return src;
-        if (!ctx->root) {                               /* a pipelined run zeroes them once */
+        if (!ctx->root)                                /* a pipelined run zeroes them once */
             HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
-            ctx->stats_stream = s;
-        }
     }
 
     /* ---- geometry ---- */
@@ -699,22 +710,17 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
              * WM_TRMAX troughs): dense only for the sorted-union kernels */
             if (need_merge && (rq_rc = interp(run, tr, ntr, wm_chunks ? WM_MMAX : INT64_MAX)) != BPMX_OK) return rq_rc;
             if (use_wm) {
-                /* pruned structure first; recordings it cannot take (too many
-                 * kept samples, > WM_TRMAX troughs) are flagged in wm_full for
-                 * the unpruned variant */
-                RollqArgs b = a;
-                if (!(P->options & BPMX_OPT_ROLLQ_NOPRUNE)) {
-                    (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds_p);
-                    LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F, (unsigned)wm_nch), dim3(WM_T), wm_lds_p, s, a,
-                           wm_pos, wm_full);
-                    b.run = wm_full;
-                    b.wm_chunk = 0;
-                }
-                (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wm_lds);
-                LAUNCH(ctx, s, "k_rollq_wm[full]", k_rollq_wm_t<false>, dim3(F), dim3(WM_T), wm_lds, s, b, wm_pos,
-                       wm_full);
+                /* the pruned structure; a recording it cannot take (too many
+                 * kept samples, > WM_TRMAX troughs, a compact-key collision)
+                 * runs unpruned in the same workgroup, so its LDS is the
+                 * larger layout (BPMX_OPT_ROLLQ_NOPRUNE: unpruned for all) */
+                wm_lds_attr();
+                if (!(P->options & BPMX_OPT_ROLLQ_NOPRUNE))
+                    LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F, (unsigned)wm_nch), dim3(WM_T),
+                           std::max(wm_lds_p, wm_lds), s, a, wm_pos, wm_full);
+                else
+                    LAUNCH(ctx, s, "k_rollq_wm[full]", k_rollq_wm_t<false>, dim3(F), dim3(WM_T), wm_lds, s, a, wm_pos,
+                           wm_full);
             }
             if (!need_merge) return BPMX_OK;
             /* long recordings: a workgroup per chunk of outputs (each chunk pays
@@ -891,7 +897,6 @@ static int run_pipelined(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *
         int64_t *d_stats = (int64_t *)ctx->buf("stats", BPMX_NSTATS * 8, &rc);
         if (rc != BPMX_OK) return rc;
         HIP_TRY(hipMemsetAsync(d_stats, 0, BPMX_NSTATS * 8, s));
-        ctx->stats_stream = s;
     }
     /* chunk boundaries by frames (recordings are whole), decimated offsets */
     const int64_t *fo = B->frame_offsets;
@@ -966,11 +971,20 @@ int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus) {
 }
 
 int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {
+    int rc;
     if (ctx && P && B && O && !ctx->root && ctx->pipe_chunks >= 2 && B->n_files >= 2 * ctx->pipe_chunks &&
         (P->stages & BPMX_STAGE_ENVELOPE) && (P->stages & (BPMX_STAGE_FLOOR | BPMX_STAGE_PEAKS)) &&
         B->frame_offsets && B->pcm && O->env && O->n_troughs && O->n_peaks && O->flags)
-        return run_pipelined(ctx, P, B, O, (hipStream_t)stream);
-    return run_impl(ctx, P, B, O, stream, false);
+        rc = run_pipelined(ctx, P, B, O, (hipStream_t)stream);
+    else
+        rc = run_impl(ctx, P, B, O, stream, false);
+    if (rc == BPMX_OK && (P->options & BPMX_OPT_STATS)) {
+        /* bpmx_stats waits for this context-owned event, not for the caller's
+         * stream, which the caller may destroy in between */
+        if (!ctx->stats_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->stats_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ctx->stats_ev, (hipStream_t)stream));
+    }
+    return rc;
 }
 
 }  // extern "C"

@@ -49,7 +49,7 @@ struct bpmx_ctx {
     bool nat_tiles_dirty = false;
     bool nat_tab_dirty = false;
     bool prof = false;
-    hipStream_t stats_stream = nullptr;          /* stream of the last run with BPMX_OPT_STATS */
+    hipEvent_t stats_ev = nullptr;               /* recorded after the last run with BPMX_OPT_STATS */
     struct Rec { std::string name; hipEvent_t a, b; };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
@@ -71,6 +71,12 @@ struct bpmx_ctx {
     }
     bool side_ready() {
         if (side[0]) return true;
+        if (root) {                     /* pipeline sub-contexts share the root context's side streams */
+            if (!root->side_ready()) return false;
+            for (int i = 0; i < NSIDE; ++i) { side[i] = root->side[i]; side_join[i] = root->side_join[i]; }
+            side_fork = root->side_fork;
+            return true;
+        }
         for (int i = 0; i < NSIDE; ++i) {
             if (hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&side_join[i], hipEventDisableTiming) != hipSuccess)

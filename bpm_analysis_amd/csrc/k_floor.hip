@@ -1169,12 +1169,15 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
         const bool und = j < jc1 && A.dec[d0 + j] == 2;
         const uint64_t bm = __ballot(und);
         if (und) s_und[__popcll(bm & ((1ull << tid) - 1ull))] = (int16_t)tid;
-        if (tid == 0) s_nund = __popcll(bm);
+        /* another workgroup of this recording may set exact[f] at any time: one
+         * read, shared, so every thread takes the same path (the value rides in
+         * the count's sign) */
+        if (tid == 0)
+            s_nund = __hip_atomic_load(&A.exact[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? -1 : __popcll(bm);
     }
     __syncthreads();
     const int nu = s_nund;
-    if (nu == 0) return;
-    if (__hip_atomic_load(&A.exact[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   /* full draft anyway */
+    if (nu <= 0) return;                                     /* none undecided, or the full draft anyway */
     const int64_t *raw = A.raw + d0;
     const double *env = A.env + d0;
     const int64_t W = A.window, t0 = raw[0];

@@ -68,32 +68,40 @@ __device__ __forceinline__ uint64_t match8(uint32_t dg) {
     return m;
 }
 
+/* returns true (uniformly) when a recording the pruned variant cannot take
+ * must be redone unpruned */
+struct RqShared {
+    int jlo, jhi, first, last, wt[WM_T / 64], mk;
+    unsigned long long orv[WM_T / 64], andv[WM_T / 64];
+    double vmin, vmax;
+};
+
 template <bool PRUNE>
-__global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full) {
+__device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch, int32_t *full, RqShared &S_) {
     constexpr int NWV = WM_T / 64;
     constexpr int MMAX = PRUNE ? WM_PMAX : WM_MMAX;          /* samples in the structure */
     constexpr int MAXIT = MMAX / WM_T;
     const int f = blockIdx.x;
-    if (f >= A.n_files) return;
+    if (f >= A.n_files) return false;
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
     if (!A.run[f]) {
         if (PRUNE && tid == 0) full[f] = 0;
-        return;
+        return false;
     }
     const int64_t d0 = A.doff[f], n = A.doff[f + 1] - d0;
     const int ntr_all = A.env ? A.ntr[f] : 0;
     /* chunk mode: a long recording's outputs [o0, o1) in workgroup (f, chunk),
      * over the samples [t0, top) their windows reach */
     const bool chunked = PRUNE && A.wm_chunk > 0 && n > WM_MMAX && A.env;
-    if (!chunked && blockIdx.y > 0) return;
+    if (!chunked && blockIdx.y > 0) return false;
     const int64_t W = A.window, minp = A.min_periods;
     int64_t o0 = 0, o1 = n, t0 = 0, top = n;
     int jlo = 0, ntr = ntr_all;                              /* troughs staged: [jlo, jlo + ntr) */
-    __shared__ int s_jlo, s_jhi;
+    int &s_jlo = S_.jlo, &s_jhi = S_.jhi;
     if (chunked) {
         if (tid == 0 && blockIdx.y == 0) full[f] = 0;        /* long: never the unpruned variant */
         o0 = (int64_t)blockIdx.y * A.wm_chunk;
-        if (o0 >= n) return;
+        if (o0 >= n) return false;
         o1 = min<int64_t>(n, o0 + A.wm_chunk);
         int64_t s, e;
         win_bounds(o0, n, W, s, e);
@@ -114,22 +122,22 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         ntr = s_jhi - s_jlo + 1;
         if (top <= t0) {                                     /* no finite sample in reach: NaN outputs */
             for (int64_t i = o0 + tid; i < o1; i += WM_T) A.out[d0 + i] = __builtin_nan("");
-            return;
+            return false;
         }
         if (top - t0 > WM_MMAX || ntr > WM_TRMAX) {
             if (tid == 0) A.wm_fail[f] = 1;
-            return;
+            return false;
         }
     }
     const bool fused = A.env && ntr <= WM_TRMAX;
     if (!chunked && (n > WM_MMAX || n <= 0 || (PRUNE && !fused))) {   /* k_rolling_quantile / the unpruned variant */
         if (PRUNE && tid == 0) full[f] = (n <= WM_MMAX && n > 0) ? 1 : 0;
-        return;
+        return PRUNE && n <= WM_MMAX && n > 0;
     }
     extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_first, s_last, s_wt[NWV], s_mk;
-    __shared__ unsigned long long s_or[NWV], s_and[NWV];
-    __shared__ double s_vmin, s_vmax;
+    int &s_first = S_.first, &s_last = S_.last, *s_wt = S_.wt, &s_mk = S_.mk;
+    unsigned long long *s_or = S_.orv, *s_and = S_.andv;
+    double &s_vmin = S_.vmin, &s_vmax = S_.vmax;
 
     const double *dense = A.dense + d0;
     double *out = A.out + d0;
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         const bool ok = span == span && span < __builtin_inf();
         if (!ok) {                                           /* non-finite curve: no pruning */
             if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
-            return;
+            return !chunked;
         }
         const double scale = span > 0.0 ? (double)NB / span : 0.0;
         /* monotone in the value: (v - vmin) * scale rounds monotonically, the
@@ -413,7 +421,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         STAMP(13);
         if (kc > WM_PMAX) {                                  /* too many kept: the unpruned variant */
             if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
-            return;
+            return !chunked;
         }
         if (tid == 0 && !chunked) full[f] = 0;
         for (int pb = wid; pb < NPB; pb += NWV) {
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
         for (int r = tid; r + 1 < m; r += WM_T) down |= svl[r] > svl[r + 1];
         if (__syncthreads_or(down)) {                        /* the full-width variant redoes it */
             if (tid == 0) { if (chunked) A.wm_fail[f] = 1; else full[f] = 1; }
-            return;
+            return !chunked;
         }
     }
     /* per-wave block scratch past the two index arrays: the collected ranks,
@@ -827,18 +835,32 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
             atomicMin(&A.vfirst[f], s_first);
             atomicMax(&A.vlast[f], s_last);
         }
-        return;
+        return false;
     }
     /* ---- .bfill().ffill() ---- */
     const int first = s_first, last = s_last;
     if (last < 0) {
         if (tid == 0) A.allnan[f] = 1;
-        return;
+        return false;
     }
     if (tid == 0) A.allnan[f] = 0;
     const double vf = out[first], vl = out[last];
     for (int64_t i = tid; i < first; i += WM_T) out[i] = vf;
     for (int64_t i = last + 1 + tid; i < n; i += WM_T) out[i] = vl;
+    return false;
+}
+
+/* The pruned variant runs a recording it cannot take (too many kept samples,
+ * a non-finite curve, a compact-key collision) through the unpruned body in
+ * the same workgroup, so no second launch is needed for it; its dynamic LDS
+ * is the larger of the two layouts. */
+template <bool PRUNE>
+__global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full) {
+    __shared__ RqShared sh;
+    if (rollq_wm_body<PRUNE>(A, pos_scratch, full, sh) && PRUNE) {
+        __syncthreads();
+        (void)rollq_wm_body<false>(A, pos_scratch, full, sh);
+    }
 }
 
 template __global__ void k_rollq_wm_t<true>(RollqArgs, uint16_t *, int32_t *);

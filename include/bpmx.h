@@ -206,8 +206,12 @@ int bpmx_profile_only(bpmx_ctx *ctx, const char *label);
  * restriction) while group k-1's detection runs beside it (on an internal
  * stream restricted to det_cus other CUs when det_cus > 0, else on the
  * caller's stream), so the HBM-bound envelope kernels overlap the
- * latency-bound detection kernels.  Same outputs as an unpipelined run.
- * chunks = 0 (the default) turns it off.  Waits for the device. */
+ * latency-bound detection kernels.  Same outputs as an unpipelined run: every
+ * index, count and flag identical; env, y and floor bit-identical in reference
+ * mode and within the native tolerance in native mode (a chunk's PCM base may
+ * lose the 16-byte alignment the int16 matrix-core block kernel needs).
+ * Pipeline sub-contexts share the root context's side streams, which carry no
+ * CU mask.  chunks = 0 (the default) turns it off.  Waits for the device. */
 int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus);
 
 /* Counters (enum bpmx_stat) of the last bpmx_run on ctx that had

@@ -1105,3 +1105,52 @@ def test_reference_split_passes_bit_identical(det):
     for f in (0, 1, 40, 69):
         o = O.detect(recs[f], fs, params, mode="reference")
         assert _same(a[f]["env"], o["env"]) and _same(a[f]["peaks"], o["peaks"]), f
+
+
+@pytest.mark.parametrize("mode", ["native", "reference"])
+def test_pipelined_run_identical(mode):
+    """bpmx_set_pipeline (envelope of chunk k beside the detection of chunk
+    k - 1, include/bpmx.h) gives the unpipelined run's outputs: troughs, peaks,
+    counts, raw-trough counts, flags and the path counters (BPMX_OPT_STATS)
+    identical, env, y and floor bit for bit in reference mode and within the
+    native tolerance in native mode (a chunk's PCM base need not be 16-byte
+    aligned, and the block kernel for int16 mono depends on that), on a ragged
+    batch with a too-short recording, with and without CU masks."""
+    import torch
+    from bpm_analysis_amd import _native as N
+    from bpm_analysis_amd.engine import Detector
+    fs = 44100
+    lens = [fs * 20, fs * 7 + 13, 146 * 15, fs * 31, fs * 12 + 5, fs * 9, fs * 25, fs * 3 + 77, fs * 16]
+    seeds = [300 + i for i in range(len(lens))]
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS, trough_rejection_multiplier=1.5)   # some undecided troughs: draft_point runs
+    ref_det = Detector(0)
+    pcm = ref_det.synth(fo, fs, 1, seeds=seeds)
+
+    def run(det):
+        r = det.run(pcm, fo, fs, params, mode=mode, want_y=True, options=N.OPT_STATS)
+        torch.cuda.synchronize()
+        return r.to_host(), det.stats(), r.n_raw_troughs.cpu().numpy().copy()
+
+    base, bst, braw = run(ref_det)
+    assert base[2]["flags"] & N.F_TOO_SHORT
+    for shape in ((2, 0, 0), (3, 0, 0), (2, 192, 64)):
+        det = Detector(0)
+        det.set_pipeline(*shape)
+        got, gst, graw = run(det)
+        assert gst == bst, shape
+        assert np.array_equal(graw, braw), shape
+        for a, b in zip(got, base):
+            assert a["flags"] == b["flags"]
+            assert a["n_raw_troughs"] == b["n_raw_troughs"]
+            for k in ("env", "y", "floor", "troughs", "peaks"):
+                if a[k] is None or b[k] is None:
+                    assert a[k] is None and b[k] is None
+                elif mode == "native" and k in ("env", "y", "floor"):
+                    scale = float(np.max(np.abs(b[k]))) or 1.0
+                    assert np.array_equal(np.isnan(a[k]), np.isnan(b[k]))
+                    assert np.nanmax(np.abs(a[k] - b[k])) <= 1e-9 * scale, (shape, k)
+                else:
+                    assert _same(a[k], b[k]), (shape, k)
+        det.close()
+    ref_det.close()

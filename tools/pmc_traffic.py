@@ -21,6 +21,10 @@ import re
 
 
 def short_name(kernel: str) -> str:
+    # torch's own kernels live in anonymous namespaces ("at::native::(anonymous
+    # namespace)::..."): drop that before cutting at the argument list (r03's
+    # summary showed the output tensors' zero fill under an empty name)
+    kernel = kernel.replace("(anonymous namespace)::", "")
     k = kernel.split("(")[0]
     full = "k_rollq_wm_t<false>" in k                 # the unpruned rolling-quantile variant
     k = re.sub(r"<.*", "", k).replace("void ", "").strip() + ("[full]" if full else "")
@@ -30,6 +34,13 @@ def short_name(kernel: str) -> str:
     return k
 
 
+# kernels launched more than once per step under different launch labels
+# (bpmx_api.hip's LAUNCH names), in launch order within a step: their
+# dispatches are labelled by their position in that cycle
+LABEL_CYCLE = {"k_find_peaks_lds": ["k_find_peaks[troughs]", "k_find_peaks[peaks]"],
+               "k_rollq_wm_t": ["k_rollq_wm[draft]", "k_rollq_wm[draft-fallback]", "k_rollq_wm[final]"]}
+
+
 def per_kernel(d: str, counter: str) -> dict:
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     acc = collections.defaultdict(list)
@@ -37,10 +48,15 @@ def per_kernel(d: str, counter: str) -> dict:
         for r in csv.DictReader(open(fn)):
             if r["Counter_Name"] != counter:
                 continue
-            acc[(r["Dispatch_Id"], short_name(r["Kernel_Name"]))].append(float(r["Counter_Value"]))
+            acc[(int(r["Dispatch_Id"]), short_name(r["Kernel_Name"]))].append(float(r["Counter_Value"]))
     by = collections.defaultdict(list)
-    for (_, k), v in acc.items():
+    seen = collections.Counter()
+    for (_, k), v in sorted(acc.items()):
         by[k].append(sum(v))            # sum over XCD / instance rows of one dispatch
+        cyc = LABEL_CYCLE.get(k)
+        if cyc:                         # also per launch label, by position in the step's cycle
+            by[cyc[seen[k] % len(cyc)]].append(sum(v))
+            seen[k] += 1
     return {k: sum(v) / len(v) for k, v in by.items()}
 
 
