@@ -210,7 +210,8 @@ __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArg
     constexpr int NW = QR_T / 64;
     __shared__ unsigned int hist[256];
     __shared__ long long s_r;
-    __shared__ int s_digit;
+    __shared__ int s_digit, s_csel, s_cc;
+    __shared__ unsigned long long s_ck[64];
     __shared__ unsigned long long s_a[NW], s_b[NW];
     __shared__ long long s_cnt[NW];
     const double INF = __builtin_inf();
@@ -282,12 +283,41 @@ __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArg
                     while (rr >= (long long)cs[d]) { rr -= cs[d]; ++d; }
                     s_digit = lane * 4 + d;
                     s_r = rr;
+                    s_csel = (int)cs[d];
                 }
+                if (lane == 0) s_cc = 0;
             }
             __syncthreads();
             prefix |= (uint64_t)s_digit << shift;
             mask |= 0xFFull << shift;
             r = s_r;
+            if (shift > 0 && s_csel <= 64) {
+                /* few keys left under the prefix (after one or two digits on
+                 * an envelope): gather them and take the r-th smallest directly
+                 * instead of the remaining digit passes */
+#pragma unroll
+                for (int it = 0; it < QR_IT; ++it) {
+                    const int64_t i = (int64_t)it * QR_T + tid;
+                    if (i < n && (key[it] & mask) == prefix) s_ck[atomicAdd(&s_cc, 1)] = key[it];
+                }
+                __syncthreads();
+                if (wid == 0) {
+                    const int c = s_cc;
+                    const unsigned long long mine = lane < c ? s_ck[lane] : ~0ull;
+                    int below = 0, same = 0;
+                    for (int j = 0; j < c; ++j) {
+                        const unsigned long long o = s_ck[j];
+                        below += o < mine;
+                        same += o == mine;
+                    }
+                    if (lane < c && below <= r && r < below + same) s_ck[0] = mine;   /* all writers agree */
+                }
+                __syncthreads();
+                prefix = s_ck[0];
+                mask = ~0ull;
+                __syncthreads();
+                break;
+            }
         }
         const double va = key_f64(prefix);
         double res = va;

@@ -712,17 +712,22 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                 }
                 /* move rs to U's Tmin-th member */
                 for (int guard = 0; guard <= m / 64 + 2; ++guard) {
-                    if (cU <= Tmin) {
+                    if (cU <= Tmin) {                        /* forward, two chunks of ranks per round trip */
                         const int rr = rs + lane;
-                        const int x = rr < m ? (int)posR[rr] : -1;
-                        const uint64_t bm = __ballot(x >= Plo && x < Phi);
-                        const int c = __popcll(bm);
-                        if (cU + c <= Tmin) {
-                            rs += 64;
-                            cU += c;
+                        const int x0 = rr < m ? (int)posR[rr] : -1;
+                        const int x1 = rr + 64 < m ? (int)posR[rr + 64] : -1;
+                        const uint64_t bm0 = __ballot(x0 >= Plo && x0 < Phi);
+                        const uint64_t bm1 = __ballot(x1 >= Plo && x1 < Phi);
+                        const int c0 = __popcll(bm0), c1 = __popcll(bm1);
+                        if (cU + c0 > Tmin) {
+                            rs += select64(bm0, Tmin - cU);
+                        } else if (cU + c0 + c1 > Tmin) {
+                            rs += 64 + select64(bm1, Tmin - cU - c0);
+                        } else {
+                            rs += 128;
+                            cU += c0 + c1;
                             continue;
                         }
-                        rs += select64(bm, Tmin - cU);
                     } else {
                         const int st = rs > 64 ? rs - 64 : 0, rr = st + lane;
                         const int x = rr < rs ? (int)posR[rr] : -1;
@@ -751,27 +756,33 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                 /* the next `need` members of U from rs, in rank order; partial ones listed */
                 int cnt = 0, np = 0;
                 const int lbase = i0 + off;                      /* member at position p: lanes [p - lbase, p - lbase + W) */
-                for (int r = rs; cnt < need && r < m; r += 64) {
+                for (int r = rs; cnt < need && r < m; r += 128) {   /* two chunks of ranks per round trip */
                     const int rr = r + lane;
-                    const int x = rr < m ? (int)posR[rr] : -1;
-                    const bool mb = x >= Plo && x < Phi;
-                    const uint64_t bm = __ballot(mb);
-                    const int slot = cnt + __popcll(bm & ltm);
-                    bool part = false;
-                    uint32_t lr = 0;
-                    if (mb && slot < need) {
-                        wl[slot] = (uint32_t)rr;
+                    const int xs[2] = {rr < m ? (int)posR[rr] : -1, rr + 64 < m ? (int)posR[rr + 64] : -1};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int x = xs[h];
+                        const bool mb = x >= Plo && x < Phi;
+                        const uint64_t bm = __ballot(mb);
+                        const int slot = cnt + __popcll(bm & ltm);
+                        /* only members within 63 indices of U's ends miss a valid lane */
+                        const bool edge = mb && slot < need && (x < PloMax || x >= PhiMin);
+                        bool part = false;
+                        uint32_t lr = 0;
+                        if (mb && slot < need) wl[slot] = (uint32_t)(rr + 64 * h);
+                        if (edge) {
                             const int pos = t0i + spos(x);
-                        const int l0 = pos - lbase, l1 = l0 + Wi - 1;
-                        const int ca = l0 > ja ? l0 : ja, cb = l1 < jb ? l1 : jb;
-                        part = ca > ja || cb < jb;
-                        /* an empty range (cb < ca) misses every lane */
-                        lr = (uint32_t)slot | ((uint32_t)(ca & 127) << 16) | ((uint32_t)((cb + 1) & 127) << 24);
+                            const int l0 = pos - lbase, l1 = l0 + Wi - 1;
+                            const int ca = l0 > ja ? l0 : ja, cb = l1 < jb ? l1 : jb;
+                            part = ca > ja || cb < jb;
+                            /* an empty range (cb < ca) misses every lane */
+                            lr = (uint32_t)slot | ((uint32_t)(ca & 127) << 16) | ((uint32_t)((cb + 1) & 127) << 24);
+                        }
+                        const uint64_t pm = __ballot(part);
+                        if (part) wpart[np + __popcll(pm & ltm)] = lr;
+                        np += __popcll(pm);
+                        cnt += __popcll(bm);
                     }
-                    const uint64_t pm = __ballot(part);
-                    if (part) wpart[np + __popcll(pm & ltm)] = lr;
-                    np += __popcll(pm);
-                    cnt += __popcll(bm);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
