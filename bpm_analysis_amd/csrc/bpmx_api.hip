@@ -356,6 +356,36 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
            d_nraw != di + 5 * F ? d_nraw : nullptr, draft_masks, bounds ? draft_vfl + 2 * F : nullptr);
 
     /* ---- ENVELOPE ---- */
+    /* the detection stage's quantile levels, built here so that the fused
+     * native Hilbert kernel can compute them from the envelope it writes */
+    QuantArgs qa{};
+    bool noise_lazy = false;
+    double *qv = nullptr;
+    if (do_floor || do_peaks) {
+        qv = (double *)ctx->buf("qv", (size_t)F * Q_SLOTS * 8, &rc);
+        if (rc != BPMX_OK) return rc;
+        qa.env = O->env; qa.doff = d_doff; qa.active = d_active; qa.n_files = F; qa.qv = qv; qa.skip_le = QR_MAX;
+        int L = 0;
+        auto add = [&](double q, int slot) {      /* one radix select per distinct level */
+            for (int l = 0; l < L; ++l)
+                if (qa.q[l] == q) { qa.slot[l] |= 1 << slot; return; }
+            qa.q[L] = q; qa.slot[L] = 1 << slot; ++L;
+        };
+        /* the noise-floor level (static fallback, < 5 troughs) is computed
+         * lazily after the trough search unless it coincides with a level
+         * needed anyway */
+        if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->fallback_q, Q_FALLBACK); }
+        if (do_peaks) add(P->peak_prom_q, Q_PEAK);
+        if (do_floor) {
+            noise_lazy = true;
+            for (int l = 0; l < L; ++l)
+                if (qa.q[l] == P->noise_floor_q) { qa.slot[l] |= 1 << Q_NOISE; noise_lazy = false; }
+        }
+        qa.n_levels = L;
+        qa.skip = nullptr;
+        qa.stats = 0;                     /* k_find_peaks builds its own block tables when it runs */
+    }
+    bool q_in_env = false;                /* every active recording's quantiles came with its envelope */
     if (do_env) {
         if (P->mode == BPMX_MODE_REFERENCE) {
             double *scr = (double *)ctx->buf("ref_scratch", (size_t)((maxnd + 30 + 63) / 64 * 64) * F * 8, &rc);
@@ -482,8 +512,13 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 HIP_TRY(hipStreamWaitEvent(s, ej, 0));
             }
         } else {
-            int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active);
+            int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active,
+                                    (do_floor || do_peaks) ? &qa : nullptr);
             if (r != BPMX_OK) return r;
+            if (do_floor || do_peaks) {
+                q_in_env = true;
+                for (int f = 0; f < F && q_in_env; ++f) q_in_env = !active[f] || ctx->nat_fused[f];
+            }
         }
     }
     if (!do_floor && !do_peaks) return BPMX_OK;
@@ -491,7 +526,6 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* ---- shared detection inputs: block tables, quantiles ---- */
     double *bmax = (double *)ctx->buf("bmax", (size_t)sumb * 8, &rc);
     double *bmin = (double *)ctx->buf("bmin", (size_t)sumb * 8, &rc);
-    double *qv = (double *)ctx->buf("qv", (size_t)F * Q_SLOTS * 8, &rc);
     int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
     int32_t *vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
     int32_t *fp_fb = (int32_t *)ctx->buf("fp_fallback", (size_t)F * 4, &rc);
@@ -548,7 +582,6 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             LAUNCH(ctx, s, "k_find_peaks[" TAG ",gm]", k_find_peaks, dim3(F), dim3(1024), 0, s, (A));     \
         }                                                                                                  \
     } while (0)
-    bool noise_lazy = false;
     if (long_files) {
         /* a few workgroups per long recording when the batch is small */
         const int64_t gy = std::min<int64_t>((((maxnd + 63) >> 6) + 3) / 4, std::max<int64_t>(1, 2048 / F));
@@ -577,28 +610,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         return BPMX_OK;
     };
     {
-        QuantArgs a;
-        a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
-        int L = 0;
-        auto add = [&](double q, int slot) {      /* one radix select per distinct level */
-            for (int l = 0; l < L; ++l)
-                if (a.q[l] == q) { a.slot[l] |= 1 << slot; return; }
-            a.q[L] = q; a.slot[L] = 1 << slot; ++L;
-        };
-        /* the noise-floor level (static fallback, < 5 troughs) is computed
-         * lazily after the trough search unless it coincides with a level
-         * needed anyway */
-        if (do_floor) { add(P->trough_prom_q, Q_TROUGH); add(P->fallback_q, Q_FALLBACK); }
-        if (do_peaks) add(P->peak_prom_q, Q_PEAK);
-        if (do_floor) {
-            noise_lazy = true;
-            for (int l = 0; l < L; ++l)
-                if (a.q[l] == P->noise_floor_q) { a.slot[l] |= 1 << Q_NOISE; noise_lazy = false; }
-        }
-        a.n_levels = L;
-        a.skip = nullptr;
-        a.stats = 0;                      /* k_find_peaks builds its own block tables when it runs */
-        LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
+        QuantArgs a = qa;
+        if (!q_in_env) LAUNCH(ctx, s, "k_quantile_reg", k_quantile_reg, dim3(F), dim3(QR_T), 0, s, a, bs);
         if (long_files) {
             /* long recordings take the noise-floor level in the same passes (one
              * more compare per key) instead of a second 15-launch round later */

@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "bpmx_kernels.h"
+
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -50,6 +52,7 @@ struct HilbArgs {
     const double2 *tabs;           /* twiddle hi [ntwh] | lo [128] | prime cos/sin tables */
     double *env;
     unsigned long long *stamps;    /* tools/hbench phase timing only (nullptr) */
+    QuantArgs q;                   /* q.n_levels > 0: also the recording's quantiles (qr_select) into q.qv */
 };
 
 __global__ void k_hilbert_env(HilbArgs A, HilbPlan P);

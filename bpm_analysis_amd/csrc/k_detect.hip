@@ -24,6 +24,7 @@
  */
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
+#include "bpmx_qsel.h"
 #include "bpmx_stamps.h"
 
 namespace bpmx {
@@ -197,9 +198,8 @@ __global__ __launch_bounds__(256) void k_block_stats(BlockStatArgs A) {
 /* k_quantile_reg: all quantile levels and the block tables of one recording
  * from a single read of env held in registers (item it of thread t is
  * position it*QR_T + t, so a wave's items of one round form one 64-sample
- * block).  Per level: MSD radix select of rank floor((n-1)q) on the
- * order-preserving keys (8-bit digits; digits constant over the recording are
- * taken from any key), then the next order statistic and numpy's _lerp. */
+ * block); the select itself is qr_select (bpmx_qsel.h), which k_hilbert_env
+ * also runs on the envelope it writes. */
 __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArgs B) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f] || (A.skip && A.skip[f])) return;
@@ -207,16 +207,9 @@ __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArg
     if (n > QR_MAX) return;
     const double *x = A.env + A.doff[f];
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-    constexpr int NW = QR_T / 64;
-    __shared__ unsigned int hist[256];
-    __shared__ long long s_r;
-    __shared__ int s_digit, s_csel, s_cc;
-    __shared__ unsigned long long s_ck[64];
-    __shared__ unsigned long long s_a[NW], s_b[NW];
-    __shared__ long long s_cnt[NW];
+    __shared__ QrShared sh;
     const double INF = __builtin_inf();
     uint64_t key[QR_IT];
-    uint64_t kor = 0, kand = ~0ull;
     double *bmx = B.bmax + B.boff[f], *bmn = B.bmin + B.boff[f];
 #pragma unroll
     for (int it = 0; it < QR_IT; ++it) {
@@ -224,131 +217,13 @@ __global__ __launch_bounds__(QR_T) void k_quantile_reg(QuantArgs A, BlockStatArg
         const bool ok = i < n;
         const double v = ok ? x[i] : 0.0;
         key[it] = ok ? f64_key(v) : 0ull;
-        if (ok) { kor |= key[it]; kand &= key[it]; }
         const int64_t b0 = (int64_t)it * QR_T + wid * 64;
         if (A.stats && b0 < n) {                             /* block max/min (k_block_stats) */
             const double mx = wave_max(ok ? v : -INF), mn = wave_min(ok ? v : INF);
             if (lane == 0) { bmx[b0 >> 6] = mx; bmn[b0 >> 6] = mn; }
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        kor |= (uint64_t)__shfl_xor((long long)kor, o);
-        kand &= (uint64_t)__shfl_xor((long long)kand, o);
-    }
-    if (lane == 0) { s_a[wid] = kor; s_b[wid] = kand; }
-    __syncthreads();
-    uint64_t vary, common;
-    {
-        uint64_t o = 0, a = ~0ull;
-        for (int w = 0; w < NW; ++w) { o |= s_a[w]; a &= s_b[w]; }
-        vary = o ^ a;
-        common = a;                                          /* the bits every key shares */
-    }
-    __syncthreads();
-    for (int l = 0; l < A.n_levels; ++l) {
-        const double q = A.q[l];
-        const double vi = (double)(n - 1) * q;
-        const bool top = vi >= (double)(n - 1);
-        const long long lo = top ? (long long)(n - 1) : (long long)floor(vi);
-        uint64_t prefix = 0, mask = 0;
-        long long r = lo;
-        for (int shift = 56; shift >= 0; shift -= 8) {
-            if (((vary >> shift) & 0xFFull) == 0) {          /* uniform: constant digit */
-                prefix |= common & (0xFFull << shift);
-                mask |= 0xFFull << shift;
-                continue;
-            }
-            if (tid < 256) hist[tid] = 0;
-            __syncthreads();
-#pragma unroll
-            for (int it = 0; it < QR_IT; ++it) {
-                const int64_t i = (int64_t)it * QR_T + tid;
-                if (i < n && (key[it] & mask) == prefix) atomicAdd(&hist[(key[it] >> shift) & 255], 1u);
-            }
-            __syncthreads();
-            if (wid == 0) {
-                const unsigned int c0 = hist[lane * 4], c1 = hist[lane * 4 + 1], c2 = hist[lane * 4 + 2],
-                                   c3 = hist[lane * 4 + 3];
-                const long long sm = (long long)c0 + c1 + c2 + c3;
-                long long incl = sm;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const long long t = __shfl_up(incl, o);
-                    if (lane >= o) incl += t;
-                }
-                const long long excl = incl - sm;
-                if (excl <= r && r < incl) {
-                    long long rr = r - excl;
-                    const unsigned int cs[4] = {c0, c1, c2, c3};
-                    int d = 0;
-                    while (rr >= (long long)cs[d]) { rr -= cs[d]; ++d; }
-                    s_digit = lane * 4 + d;
-                    s_r = rr;
-                    s_csel = (int)cs[d];
-                }
-                if (lane == 0) s_cc = 0;
-            }
-            __syncthreads();
-            prefix |= (uint64_t)s_digit << shift;
-            mask |= 0xFFull << shift;
-            r = s_r;
-            if (shift > 0 && s_csel <= 64) {
-                /* few keys left under the prefix (after one or two digits on
-                 * an envelope): gather them and take the r-th smallest directly
-                 * instead of the remaining digit passes */
-#pragma unroll
-                for (int it = 0; it < QR_IT; ++it) {
-                    const int64_t i = (int64_t)it * QR_T + tid;
-                    if (i < n && (key[it] & mask) == prefix) s_ck[atomicAdd(&s_cc, 1)] = key[it];
-                }
-                __syncthreads();
-                if (wid == 0) {
-                    const int c = s_cc;
-                    const unsigned long long mine = lane < c ? s_ck[lane] : ~0ull;
-                    int below = 0, same = 0;
-                    for (int j = 0; j < c; ++j) {
-                        const unsigned long long o = s_ck[j];
-                        below += o < mine;
-                        same += o == mine;
-                    }
-                    if (lane < c && below <= r && r < below + same) s_ck[0] = mine;   /* all writers agree */
-                }
-                __syncthreads();
-                prefix = s_ck[0];
-                mask = ~0ull;
-                __syncthreads();
-                break;
-            }
-        }
-        const double va = key_f64(prefix);
-        double res = va;
-        if (!top) {
-            unsigned long long mn = ~0ull;
-            long long cnt = 0;
-#pragma unroll
-            for (int it = 0; it < QR_IT; ++it) {
-                const int64_t i = (int64_t)it * QR_T + tid;
-                if (i < n) {
-                    if (key[it] <= prefix) cnt++;
-                    else if (key[it] < mn) mn = key[it];
-                }
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long om = __shfl_xor(mn, o);
-                mn = om < mn ? om : mn;
-                cnt += __shfl_xor(cnt, o);
-            }
-            __syncthreads();
-            if (lane == 0) { s_a[wid] = mn; s_cnt[wid] = cnt; }
-            __syncthreads();
-            unsigned long long m = s_a[0];
-            long long c = 0;
-            for (int w = 0; w < NW; ++w) { m = s_a[w] < m ? s_a[w] : m; c += s_cnt[w]; }
-            const double vb = (c > lo + 1) ? va : key_f64(m);
-            res = np_lerp(va, vb, vi - (double)lo);
-        }
-        if (tid < Q_SLOTS && ((A.slot[l] >> tid) & 1)) A.qv[(int64_t)f * Q_SLOTS + tid] = res;
-        __syncthreads();
-    }
+    qr_select(key, n, A, f, sh);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -41,6 +41,7 @@
 #include "bpmx_kernels.h"
 #include "bpmx_native.h"
 #include "bpmx_hilbert.h"
+#include "bpmx_qsel.h"
 #include "bpmx_xlane.h"
 
 namespace bpmx {
@@ -1814,7 +1815,7 @@ HbTables *hb_tables(bpmx_ctx *ctx, int64_t nd, int window, HilbPlan *P, size_t *
 
 int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
-                    const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active) {
+                    const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active, const QuantArgs *qa) {
     const int ds = P->ds;
     if (ds > NAT_DSMAX) return fail(BPMX_E_LIMIT, "native mode supports ds <= " + std::to_string(NAT_DSMAX));
     int rc = BPMX_OK;
@@ -2032,6 +2033,11 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 HilbArgs a;
                 a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
                 a.tabs = ht->dev; a.env = O->env; a.stamps = nullptr;
+                a.q = QuantArgs{};
+                if (qa) {
+                    a.q = *qa;                                   /* the select's scratch is the stage region */
+                    hlds = std::max(hlds, sizeof(QrShared));
+                }
                 (void)hipFuncSetAttribute((const void *)k_hilbert_env, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)hlds);
                 LAUNCH(ctx, s, "k_hilbert_env", k_hilbert_env, dim3((unsigned)(f1 - f0)), dim3(HB_T), hlds, s, a, hp);

@@ -27,6 +27,7 @@
  */
 #include "bpmx_common.h"
 #include "bpmx_hilbert.h"
+#include "bpmx_qsel.h"
 #include "bpmx_stamps.h"
 
 namespace bpmx {
@@ -430,6 +431,8 @@ __device__ __forceinline__ int hb_pos(const HilbPlan &P, int k) {     /* positio
     return pos;
 }
 
+static_assert(HB_T == QR_T, "k_hilbert_env runs qr_select with its own threads");
+
 __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     const int f = A.f_begin + blockIdx.x;
     if (f >= A.f_end || !A.active[f]) return;
@@ -577,6 +580,18 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         if (i0 + j < i1) stage[i0 + j] = ev[j];
     __syncthreads();
     for (int i = threadIdx.x; i < N; i += HB_T) env[i] = stage[i];
+    if (A.q.n_levels > 0 && N <= QR_MAX) {
+        /* the detection stage's quantiles from the staged envelope (the same
+         * doubles just stored), so k_quantile_reg need not reload it */
+        uint64_t key[QR_IT];
+#pragma unroll
+        for (int it = 0; it < QR_IT; ++it) {
+            const int i = it * HB_T + (int)threadIdx.x;
+            key[it] = i < N ? f64_key(stage[i]) : 0ull;
+        }
+        __syncthreads();                                    /* the stage becomes the select's scratch */
+        qr_select(key, N, A.q, f, *reinterpret_cast<QrShared *>(hb_smem));
+    }
     __syncthreads();
     STAMP(7);
     STAMP_FLUSH(A.stamps);

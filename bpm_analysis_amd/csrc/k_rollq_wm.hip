@@ -431,6 +431,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
         m = kc;
         __syncthreads();
     }
+#ifdef RQ_STOP_PRUNE
+    return false;                                            /* tools/rqbench phase-truncated diagnostic builds */
+#endif
     /* relative position of the c-th sample in the structure */
     auto spos = [&](int c) -> int { return PRUNE ? (int)kpos[c] : c; };
     /* structure index range of relative positions [0, p) */
@@ -605,6 +608,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     /* per-wave block scratch past the two index arrays: the collected ranks,
      * then the partial members; the sorted values past that when they fit
      * (else each output evaluates its two) */
+#ifdef RQ_STOP_SORT
+    return false;
+#endif
     uint32_t *wl = (uint32_t *)(smem + Lay.area + wsc) + (size_t)wid * WM_WSCR;
     STAMP(5);
 
@@ -839,7 +845,7 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     }
     __threadfence_block();
     __syncthreads();
-    STAMP(6);
+    STAMP(7);                                                /* (the other waves' query tail) */
     STAMP_FLUSH(A.stamps);
     if (chunked) {                                           /* bfill / ffill over all chunks: k_rollq_fill */
         if (tid == 0 && s_last >= 0) {

@@ -84,7 +84,7 @@ int main(int argc, char **argv) {
     double sum[16] = {0};
     for (int f = 0; f < F; ++f)
         for (int k = 0; k < 16; ++k) sum[k] += (double)st[(size_t)f * 16 + k];
-    const char *names[16] = {"load", "count", "scan", "exchange", "q:bounds", "build", "q:skip+out", "compact",
+    const char *names[16] = {"load", "count", "scan", "exchange", "q:bounds", "build", "q:skip+out", "cmpct+wait",
                              "p:tables", "p:hist", "p:prefix", "p:bstar", "p:thr", "p:keep", "q:cursor", "q:collect"};
     double tot = 0;
     for (int k = 0; k < 16; ++k) tot += sum[k];
@@ -105,6 +105,9 @@ int main(int argc, char **argv) {
            (long)nd, lds, best, tot / F, nfull);
     for (int k = 0; k < 16; ++k)
         if (sum[k] > 0) printf("   %-10s %12.0f  %5.1f%%\n", names[k], sum[k] / F, 100.0 * sum[k] / tot);
+#if defined(RQ_STOP_PRUNE) || defined(RQ_STOP_SORT)
+    return 0;                                                /* phase-truncated diagnostic build: no outputs */
+#endif
     std::vector<double> o(N);
     CK(hipMemcpy(o.data(), d_out, N * 8, hipMemcpyDeviceToHost));
     long bad = 0, checked = 0;
