@@ -327,7 +327,7 @@ constexpr int WM_PMAX = 12288;               /* kept samples of the pruned varia
  * runs as four passes of 16), then as many partial-member records.  Small,
  * so that the sorted values fit beside it up to ~8000 kept samples. */
 constexpr int WM_DCAP = 96;
-constexpr int WM_WSCR = 2 * WM_DCAP;
+constexpr int WM_WSCR = WM_DCAP;              /* per-wave scratch of the output phase: the collected ranks */
 /* dynamic LDS of k_rollq_wm_t: trough tables | (pruned) kept masks, prefix,
  * bins | (pruned) kept positions | phase area (histogram / sort / matrix) */
 struct WmLayout {

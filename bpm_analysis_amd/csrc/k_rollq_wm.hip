@@ -33,9 +33,9 @@
  *      atomic, issued in slot order) + peers below in the same round (ballot
  *      match) + one (digit, wave) block scan.
  *   2. outputs, 64 consecutive ones per wave step: a rank cursor moved from
- *      block to block, the block's candidate ranks collected from it, and each
- *      lane's k-th / (k+1)-th smallest selected from a transposed 64 x 64
- *      membership bit matrix (details at the phase).  pandas' linear
+ *      block to block, the block's candidate members collected from it in rank
+ *      order until every lane's k-th / (k+1)-th own member is among them, each
+ *      lane skipping the few members its window misses (details at the phase).  pandas' linear
  *      interpolation, nobs / min_periods from the window bounds.  NaN outputs
  *      are a prefix and a suffix (nobs is unimodal), filled from the first and
  *      last valid output.  (r01-r03 answered every output by a top-down descent
@@ -647,8 +647,10 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     };
     const uint64_t ltm = lanemask_lt();
     const int off = (int)((W - 1) / 2), Wi = (int)W, ni = (int)n, t0i = (int)t0;
+#ifdef RQ_DIAG_Q
+    unsigned long long dq[8] = {0};   /* tools/rqbench -DRQ_DIAG_Q, wave 0: blocks, need, partial members, collect trips, cursor trips, collected */
+#endif
     int vfirst = INT_MAX, vlast = -1;
-    uint32_t *wpart = wl + WM_DCAP;                          /* partial members: L index | lane range */
     {
         const int NBLK = (int)((o1 - o0 + 63) >> 6);
         const int NBW = (NBLK + NWV - 1) / NWV;
@@ -689,6 +691,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             int Tmin = -wave_max_dpp(valid ? -t : INT_MIN + 1);
             int need = wave_max_dpp(valid ? t - Tmin + (plo - Plo) + (Phi - phi) : 0) + 2;
             const int npass = need > WM_DCAP ? 4 : 1;
+#ifdef RQ_DIAG_Q
+            dq[0] += 1; dq[1] += (unsigned long long)need;
+#endif
 #ifdef BPMX_STAMPS
             if (threadIdx.x == 0) _st_acc[12] += 1000000ull * (npass > 1) + (unsigned long long)need;   /* diagnostics: 4-pass blocks, need */
 #endif
@@ -718,6 +723,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                 }
                 /* move rs to U's Tmin-th member */
                 for (int guard = 0; guard <= m / 64 + 2; ++guard) {
+#ifdef RQ_DIAG_Q
+                    dq[4] += 1;
+#endif
                     if (cU <= Tmin) {                        /* forward, two chunks of ranks per round trip */
                         const int rr = rs + lane;
                         const int x0 = rr < m ? (int)posR[rr] : -1;
@@ -759,14 +767,25 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                     na = t - Tmin + __popcll(mL & ((1ull << dl) - 1ull)) + __popcll(mR >> dr);
                 }
                 STAMP(14);
-                /* the next `need` members of U from rs, in rank order; partial ones listed */
-                int cnt = 0, np = 0;
+                /* the next members of U from rs, in rank order (at most `need`).
+                 * The partial ones (they miss some valid lane) are taken in slot
+                 * order as they come, each lane skipping those it misses while
+                 * locating its na-th own member (ia) and the next (ib); once every
+                 * valid lane's ib lies below the count collected, later members
+                 * cannot move either, so the walk stops there (usually within the
+                 * first 64 ranks; `need` bounds it in any case). */
+                int cnt = 0, ia = na, ib = -1;
                 const int lbase = i0 + off;                      /* member at position p: lanes [p - lbase, p - lbase + W) */
-                for (int r = rs; cnt < need && r < m; r += 128) {   /* two chunks of ranks per round trip */
+                bool more = true;
+                for (int r = rs; more && cnt < need && r < m; r += 128) {   /* two chunks of ranks per round trip */
+#ifdef RQ_DIAG_Q
+                    dq[3] += 1;
+#endif
                     const int rr = r + lane;
                     const int xs[2] = {rr < m ? (int)posR[rr] : -1, rr + 64 < m ? (int)posR[rr + 64] : -1};
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
+                        if (!more || cnt >= need) break;         /* uniform */
                         const int x = xs[h];
                         const bool mb = x >= Plo && x < Phi;
                         const uint64_t bm = __ballot(mb);
@@ -784,32 +803,33 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                             /* an empty range (cb < ca) misses every lane */
                             lr = (uint32_t)slot | ((uint32_t)(ca & 127) << 16) | ((uint32_t)((cb + 1) & 127) << 24);
                         }
-                        const uint64_t pm = __ballot(part);
-                        if (part) wpart[np + __popcll(pm & ltm)] = lr;
-                        np += __popcll(pm);
                         cnt += __popcll(bm);
+                        for (uint64_t pm = __ballot(part); pm; pm &= pm - 1) {   /* slot order = lane order */
+                            const uint32_t pr = (uint32_t)__builtin_amdgcn_readlane((int)lr, __ffsll((long long)pm) - 1);
+                            const int li = (int)(pr & 0xFFFFu), ca = (int)((pr >> 16) & 127u), cb1 = (int)(pr >> 24);
+                            const bool miss = lane < ca || lane >= cb1;
+#ifdef RQ_DIAG_Q
+                            dq[2] += 1;
+#endif
+                            if (ib < 0) {
+                                if (li <= ia) {
+                                    if (miss) ++ia;
+                                    continue;
+                                }
+                                ib = ia + 1;
+                            }
+                            if (li == ib && miss) ++ib;
+                        }
+                        more = __ballot(valid && (ib >= 0 ? ib : ia + 1) >= cnt) != 0;
                     }
                 }
+#ifdef RQ_DIAG_Q
+                dq[5] += (unsigned long long)cnt;
+#endif
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 STAMP(15);
-                /* this lane's na-th own member and the next: skip the partial ones it
-                 * misses (usually none or one or two per block) */
-                int ia = na, ib = -1;
-                for (int u = 0; u < np; ++u) {
-                    const uint32_t pr = wpart[u];
-                    const int li = (int)(pr & 0xFFFFu), ca = (int)((pr >> 16) & 127u), cb1 = (int)(pr >> 24);
-                    const bool miss = lane < ca || lane >= cb1;
-                    if (ib < 0) {
-                        if (li <= ia) {
-                            if (miss) ++ia;
-                            continue;
-                        }
-                        ib = ia + 1;
-                    }
-                    if (li == ib && miss) ++ib;
-                }
                 if (ib < 0) ib = ia + 1;
                 ia = ia < need ? ia : need - 1;                  /* (never binds; keeps a corrupted walk in bounds) */
                 ib = ib < need ? ib : need - 1;
@@ -847,6 +867,10 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     __syncthreads();
     STAMP(7);                                                /* (the other waves' query tail) */
     STAMP_FLUSH(A.stamps);
+#ifdef RQ_DIAG_Q
+    if (threadIdx.x == 0 && A.stamps)
+        for (int k = 0; k < 8; ++k) A.stamps[blockIdx.x * 16 + 8 + k] = dq[k];
+#endif
     if (chunked) {                                           /* bfill / ffill over all chunks: k_rollq_fill */
         if (tid == 0 && s_last >= 0) {
             atomicMin(&A.vfirst[f], s_first);

@@ -4,6 +4,10 @@
  * checked bit for bit against the library's floor.
  *   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off [-DVARIANT...] tools/rqbench.hip -o tools/rqbench
  *   python tools/dump_floor_inputs.py 1024 native /tmp/floor_in.bin && ./tools/rqbench /tmp/floor_in.bin
+ * Diagnostic builds: -DRQ_STOP_PRUNE / -DRQ_STOP_SORT end the kernel after
+ * the pruning / the sort (phase costs by difference, e.g. with rocprofv3
+ * --pmc SQ_INSTS_VALU; no output check), -DRQ_DIAG_Q prints per-block
+ * statistics of the output phase (need, partial members, trips).
  */
 #define BPMX_STAMPS 1
 #include "../bpm_analysis_amd/csrc/k_rollq_wm.hip"
@@ -95,6 +99,15 @@ int main(int argc, char **argv) {
         std::sort(ms.begin(), ms.end());
         printf("kept samples m: min %llu p10 %llu p50 %llu p90 %llu p99 %llu max %llu\n", ms[0], ms[F / 10], ms[F / 2],
                ms[F * 9 / 10], ms[F * 99 / 100], ms[F - 1]);
+    }
+#endif
+#ifdef RQ_DIAG_Q
+    {
+        double a[8] = {0};
+        for (int f = 0; f < F; ++f)
+            for (int k = 0; k < 8; ++k) a[k] += (double)st[(size_t)f * 16 + 8 + k];
+        printf("wave 0 per block: need %.2f, partial members %.2f, collect trips %.2f, cursor trips %.2f, collected %.2f (%.0f blocks)\n",
+               a[1] / a[0], a[2] / a[0], a[3] / a[0], a[4] / a[0], a[5] / a[0], a[0]);
     }
 #endif
     std::vector<int32_t> fl(F);
