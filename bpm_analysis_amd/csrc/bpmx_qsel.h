@@ -19,9 +19,10 @@
 
 namespace bpmx {
 
-/* workgroup scratch (LDS) of the select; ~2.7 KB */
+/* workgroup scratch (LDS) of the select; ~3.7 KB */
 struct QrShared {
     unsigned int hist[256];
+    unsigned int hist0[256];       /* the first varying digit's histogram: the same for every level */
     long long r;
     int digit, csel, cc;
     unsigned long long ck[64];
@@ -55,6 +56,21 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
         common = a;                                          /* the bits every key shares */
     }
     __syncthreads();
+    /* every level's first pass has no prefix yet: one histogram of the
+     * highest varying digit serves them all */
+    int shift0 = -1;
+    for (int sh = 56; sh >= 0; sh -= 8)
+        if ((vary >> sh) & 0xFFull) { shift0 = sh; break; }
+    if (shift0 >= 0) {
+        if (tid < 256) S.hist0[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < QR_IT; ++it) {
+            const int64_t i = (int64_t)it * QR_T + tid;
+            if (i < n) atomicAdd(&S.hist0[(key[it] >> shift0) & 255], 1u);
+        }
+        __syncthreads();
+    }
     for (int l = 0; l < A.n_levels; ++l) {
         const double q = A.q[l];
         const double vi = (double)(n - 1) * q;
@@ -68,17 +84,19 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
                 mask |= 0xFFull << shift;
                 continue;
             }
-            if (tid < 256) S.hist[tid] = 0;
-            __syncthreads();
+            const unsigned int *hs = shift == shift0 ? S.hist0 : S.hist;   /* uniform */
+            if (shift != shift0) {
+                if (tid < 256) S.hist[tid] = 0;
+                __syncthreads();
 #pragma unroll
-            for (int it = 0; it < QR_IT; ++it) {
-                const int64_t i = (int64_t)it * QR_T + tid;
-                if (i < n && (key[it] & mask) == prefix) atomicAdd(&S.hist[(key[it] >> shift) & 255], 1u);
+                for (int it = 0; it < QR_IT; ++it) {
+                    const int64_t i = (int64_t)it * QR_T + tid;
+                    if (i < n && (key[it] & mask) == prefix) atomicAdd(&S.hist[(key[it] >> shift) & 255], 1u);
+                }
+                __syncthreads();
             }
-            __syncthreads();
             if (wid == 0) {
-                const unsigned int c0 = S.hist[lane * 4], c1 = S.hist[lane * 4 + 1], c2 = S.hist[lane * 4 + 2],
-                                   c3 = S.hist[lane * 4 + 3];
+                const unsigned int c0 = hs[lane * 4], c1 = hs[lane * 4 + 1], c2 = hs[lane * 4 + 2], c3 = hs[lane * 4 + 3];
                 const long long sm = (long long)c0 + c1 + c2 + c3;
                 long long incl = sm;
                 for (int o = 1; o < 64; o <<= 1) {

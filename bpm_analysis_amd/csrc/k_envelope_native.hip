@@ -41,6 +41,9 @@
 #include "bpmx_kernels.h"
 #include "bpmx_native.h"
 #include "bpmx_hilbert.h"
+#ifndef BPMX_NM_POLICY
+#define BPMX_NM_POLICY ""   /* cache policy of the metric block kernel's PCM stream (A/B: " nt") */
+#endif
 #include "bpmx_qsel.h"
 #include "bpmx_xlane.h"
 
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
              * read, draining the other slot's DMA too.  The waits are explicit
              * (vmcnt below); a compiler-generated wait can only over-wait. */
             const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(slot + r * 64);
-            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" BPMX_NM_POLICY
                          :: "v"(pcm + c), "s"(m0) : "memory");
         }
     };
