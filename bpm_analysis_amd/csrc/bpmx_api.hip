@@ -529,6 +529,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
     int32_t *vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
     int32_t *fp_fb = (int32_t *)ctx->buf("fp_fallback", (size_t)F * 4, &rc);
+    /* the trough search's scan of env, reused by the peak search of the same run */
+    int32_t *fp_scan = (int32_t *)ctx->buf("fp_scan", (size_t)F * 4 * (1 + 2 * (1024 / 64)), &rc);
     uint8_t *state = (uint8_t *)ctx->buf("state", (size_t)sumnd, &rc);
     if (rc != BPMX_OK) return rc;
     BlockStatArgs bs;
@@ -637,6 +639,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5; a.tie_bit = BPMX_F_TROUGH_TIE;
+            a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F; a.reuse_scan = 0;
             FIND_PEAKS(a, "troughs");
         }
         if (bad_window)
@@ -828,6 +831,9 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0; a.tie_bit = BPMX_F_PEAK_TIE;
+        if (do_floor) {                   /* the trough launch above recorded its scan (scan_ok per recording) */
+            a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F; a.reuse_scan = 1;
+        }
         FIND_PEAKS(a, "peaks");
     }
 #undef FIND_PEAKS

@@ -121,6 +121,14 @@ struct PeakArgs {
     int64_t lds_nmax;      /* k_find_peaks_lds: hand recordings longer than this over (fallback = 1) */
     int32_t *flags;        /* [F] per-file flags: tie_bit is OR'd in when the distance filter met a decisive tie */
     int32_t tie_bit;       /* BPMX_F_TROUGH_TIE or BPMX_F_PEAK_TIE */
+    /* k_find_peaks_lds over the same envelope twice (troughs, then peaks): the
+     * trough launch records its scan — per recording scan_ok, per wave the
+     * counts of its maxima and valleys (cand / vcand runs) — and the peak
+     * launch (reuse_scan) takes the valleys as its maxima and the maxima as
+     * its valleys instead of scanning again */
+    int32_t *scan_ok = nullptr;    /* [F] */
+    int32_t *scan_cnt = nullptr;   /* [F][FP_T / 64][2] */
+    int32_t reuse_scan = 0;
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif

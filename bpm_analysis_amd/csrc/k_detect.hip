@@ -608,14 +608,22 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files) return;
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+    const bool reuse = A.reuse_scan && A.scan_ok[f];         /* the trough launch's scan of this envelope */
+    const bool record = !A.reuse_scan && A.scan_ok;
     if (!A.active[f]) {
-        if (tid == 0) A.fallback[f] = 0;
+        if (tid == 0) {
+            A.fallback[f] = 0;
+            if (record) A.scan_ok[f] = 0;
+        }
         return;
     }
     const int64_t d0 = A.doff[f];
     const int64_t n = A.doff[f + 1] - d0;
     if (n > A.lds_nmax) {                                    /* long recording: the k_fpl_* kernels */
-        if (tid == 0) A.fallback[f] = 1;
+        if (tid == 0) {
+            A.fallback[f] = 1;
+            if (record) A.scan_ok[f] = 0;
+        }
         return;
     }
     const double *e = A.env + d0;
@@ -649,6 +657,14 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     int32_t *mp_g = A.cand + d0, *vp_g = A.vcand + d0;
     int cm = 0, cv = 0;                                      /* wave-uniform counts */
     const unsigned long long lt = (1ull << lane) - 1ull;
+    if (reuse) {
+        /* -env's valleys are env's maxima (plateau midpoints, below) and its
+         * maxima env's valleys: the same positions in the same per-wave runs */
+        mp_g = A.vcand + d0;
+        vp_g = A.cand + d0;
+        cm = A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1];
+        cv = A.scan_cnt[((int64_t)f * NW + wid) * 2];
+    } else {
     /* one coalesced load per 64 positions, issued a block ahead; the left and
      * right neighbours come from the adjacent lanes (DPP wave shifts), the
      * block edges from the previous / next block's end lanes */
@@ -671,8 +687,10 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
                     while (ia < n - 1 && sg * e[ia] == xi) ia++;
                     xr = sg * e[ia];
                 }
+                /* a valley's plateau midpoint too (its value is the plateau's):
+                 * the other sign's launch takes it as a maximum */
                 if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
-                else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)i; }
+                else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)((i + ia - 1) >> 1); }
             }
         }
         const unsigned long long bm = __ballot(ism), bv = __ballot(isv);
@@ -683,6 +701,11 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         xedge = __shfl(xc, 63);
         xc = xn;
     }
+    if (record && lane == 0) {
+        A.scan_cnt[((int64_t)f * NW + wid) * 2] = cm;
+        A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1] = cv;
+    }
+    }
     if (lane == 0) { s_gc[0][0][wid] = cm; s_gc[1][0][wid] = cv; }
     __syncthreads();
     int M = 0, om = 0;
@@ -692,10 +715,16 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     }
     STAMP(1);
     if (M > FL_MC) {                                         /* k_find_peaks takes this recording */
-        if (tid == 0) A.fallback[f] = 1;
+        if (tid == 0) {
+            A.fallback[f] = 1;
+            if (record) A.scan_ok[f] = 0;
+        }
         return;
     }
-    if (tid == 0) A.fallback[f] = 0;
+    if (tid == 0) {
+        A.fallback[f] = 0;
+        if (record) A.scan_ok[f] = 1;
+    }
     const int64_t dist = A.distance;
     for (int t = lane; t < cm; t += 64) {                    /* this wave's run of maxima */
         const int32_t p = mp_g[w0 - 1 + t];
