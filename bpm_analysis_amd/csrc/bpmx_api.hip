@@ -28,6 +28,7 @@
 #include "bpmx_kernels.h"
 #include "bpmx_ctx.h"
 #include "bpmx_native.h"
+#include "bpmx_fpscan.h"
 #include "bpmx_synth.h"
 
 using namespace bpmx;
@@ -46,7 +47,7 @@ namespace {
  * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
 __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *active, int32_t *flags, int32_t *ntr,
                                                   int32_t *npk, int32_t *runs, int32_t *nraw, int32_t *z1,
-                                                  int32_t *z2) {
+                                                  int32_t *z2, int32_t *z3) {
     const int f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n_files) return;
     flags[f] = active[f] ? 0 : BPMX_F_TOO_SHORT;
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *ac
     if (nraw) nraw[f] = 0;                                   /* the caller's raw-trough counts */
     if (z1) z1[f] = 0;                                       /* draft exact masks (one int per recording) */
     if (z2) { z2[f] = 0; z2[n_files + f] = 0; }              /* draft undecided counters nund[f], nund[F + f] */
+    if (z3) z3[f] = 0;                                       /* find_peaks' scan record: none yet in this run */
 }
 
 /* recordings with >= 5 raw troughs reach the rolling quantile: with a noise
@@ -351,9 +353,18 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         draft_vfl = (int32_t *)ctx->buf("draft_vfl", (size_t)F * 16, &rc);
         if (rc != BPMX_OK) return rc;
     }
+    /* find_peaks' candidate lists and the run's scan record (bpmx_fpscan.h:
+     * the trough launch's scan, reused by the peak launch) */
+    int32_t *cand = nullptr, *vcand = nullptr, *fp_scan = nullptr;
+    if (do_floor || do_peaks) {
+        cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
+        vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
+        fp_scan = (int32_t *)ctx->buf("fp_scan", (size_t)F * 4 * (1 + 2 * FPS_NW), &rc);
+        if (rc != BPMX_OK) return rc;
+    }
     LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, F, d_active, (int32_t *)O->flags,
            do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1,
-           d_nraw != di + 5 * F ? d_nraw : nullptr, draft_masks, bounds ? draft_vfl + 2 * F : nullptr);
+           d_nraw != di + 5 * F ? d_nraw : nullptr, draft_masks, bounds ? draft_vfl + 2 * F : nullptr, fp_scan);
 
     /* ---- ENVELOPE ---- */
     /* the detection stage's quantile levels, built here so that the fused
@@ -526,11 +537,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* ---- shared detection inputs: block tables, quantiles ---- */
     double *bmax = (double *)ctx->buf("bmax", (size_t)sumb * 8, &rc);
     double *bmin = (double *)ctx->buf("bmin", (size_t)sumb * 8, &rc);
-    int32_t *cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
-    int32_t *vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
     int32_t *fp_fb = (int32_t *)ctx->buf("fp_fallback", (size_t)F * 4, &rc);
-    /* the trough search's scan of env, reused by the peak search of the same run */
-    int32_t *fp_scan = (int32_t *)ctx->buf("fp_scan", (size_t)F * 4 * (1 + 2 * (1024 / 64)), &rc);
     uint8_t *state = (uint8_t *)ctx->buf("state", (size_t)sumnd, &rc);
     if (rc != BPMX_OK) return rc;
     BlockStatArgs bs;
@@ -639,7 +646,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5; a.tie_bit = BPMX_F_TROUGH_TIE;
-            a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F; a.reuse_scan = 0;
+            a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;
             FIND_PEAKS(a, "troughs");
         }
         if (bad_window)
@@ -831,9 +838,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0; a.tie_bit = BPMX_F_PEAK_TIE;
-        if (do_floor) {                   /* the trough launch above recorded its scan (scan_ok per recording) */
-            a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F; a.reuse_scan = 1;
-        }
+        a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;   /* the run's scan record: Hilbert's or the trough launch's */
         FIND_PEAKS(a, "peaks");
     }
 #undef FIND_PEAKS

@@ -121,14 +121,12 @@ struct PeakArgs {
     int64_t lds_nmax;      /* k_find_peaks_lds: hand recordings longer than this over (fallback = 1) */
     int32_t *flags;        /* [F] per-file flags: tie_bit is OR'd in when the distance filter met a decisive tie */
     int32_t tie_bit;       /* BPMX_F_TROUGH_TIE or BPMX_F_PEAK_TIE */
-    /* k_find_peaks_lds over the same envelope twice (troughs, then peaks): the
-     * trough launch records its scan — per recording scan_ok, per wave the
-     * counts of its maxima and valleys (cand / vcand runs) — and the peak
-     * launch (reuse_scan) takes the valleys as its maxima and the maxima as
-     * its valleys instead of scanning again */
+    /* the run's extrema scan record (bpmx_fpscan.h): ok[f] = +1 / -1 when
+     * k_hilbert_env or an earlier find_peaks launch of this run left the
+     * lists in cand / vcand (made for x = +env / -env), 0 = scan here (and
+     * record); null: no record */
     int32_t *scan_ok = nullptr;    /* [F] */
-    int32_t *scan_cnt = nullptr;   /* [F][FP_T / 64][2] */
-    int32_t reuse_scan = 0;
+    int32_t *scan_cnt = nullptr;   /* [F][FPS_NW][2] */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif

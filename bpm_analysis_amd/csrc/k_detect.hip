@@ -25,6 +25,7 @@
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 #include "bpmx_qsel.h"
+#include "bpmx_fpscan.h"
 #include "bpmx_stamps.h"
 
 namespace bpmx {
@@ -608,24 +609,18 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files) return;
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-    const bool reuse = A.reuse_scan && A.scan_ok[f];         /* the trough launch's scan of this envelope */
-    const bool record = !A.reuse_scan && A.scan_ok;
     if (!A.active[f]) {
-        if (tid == 0) {
-            A.fallback[f] = 0;
-            if (record) A.scan_ok[f] = 0;
-        }
+        if (tid == 0) A.fallback[f] = 0;
         return;
     }
     const int64_t d0 = A.doff[f];
     const int64_t n = A.doff[f + 1] - d0;
     if (n > A.lds_nmax) {                                    /* long recording: the k_fpl_* kernels */
-        if (tid == 0) {
-            A.fallback[f] = 1;
-            if (record) A.scan_ok[f] = 0;
-        }
+        if (tid == 0) A.fallback[f] = 1;
         return;
     }
+    const int sgn = A.sign > 0 ? 1 : -1;
+    const int so = A.scan_ok ? A.scan_ok[f] : 0;             /* this run's scan record (read before tid 0 updates it) */
     const double *e = A.env + d0;
     const double *h = A.height ? A.height + d0 : nullptr;
     const double sg = A.sign;
@@ -646,65 +641,34 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     __shared__ int s_tie;
     STAMP_DECL
 
-    /* (1) local maxima (plateau midpoints) and valley starts, in order: wave w
+    /* (1) local maxima (plateau midpoints) and valleys, in order: wave w
      * scans its own contiguous run of positions 64 at a time (coalesced loads,
      * no workgroup barrier), compacting its hits into its own stretch of the
      * global scratch (a run of c positions holds at most c hits); one scan of
-     * the 16 per-wave counts then places every run */
-    const int64_t span = n > 2 ? n - 2 : 0;                  /* positions 1 .. n-2 */
-    const int64_t chunk = ((span + NW - 1) / NW + 63) & ~(int64_t)63;
-    const int64_t w0 = 1 + (int64_t)wid * chunk, w1 = min<int64_t>(n - 1, w0 + chunk);
-    int32_t *mp_g = A.cand + d0, *vp_g = A.vcand + d0;
-    int cm = 0, cv = 0;                                      /* wave-uniform counts */
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    if (reuse) {
-        /* -env's valleys are env's maxima (plateau midpoints, below) and its
-         * maxima env's valleys: the same positions in the same per-wave runs */
-        mp_g = A.vcand + d0;
-        vp_g = A.cand + d0;
-        cm = A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1];
-        cv = A.scan_cnt[((int64_t)f * NW + wid) * 2];
+     * the 16 per-wave counts then places every run (bpmx_fpscan.h).  When this
+     * run's scan record holds the lists (k_hilbert_env, or the trough launch
+     * for the peak launch) they are taken as they are, swapped for the other
+     * sign: -env's maxima are env's valleys and its valleys env's maxima. */
+    static_assert(NW == FPS_NW, "the scan record's per-wave runs");
+    int64_t w0, w1;
+    fp_scan_run(n, wid, w0, w1);
+    int32_t *mp_g, *vp_g;
+    int cm, cv;                                              /* wave-uniform counts */
+    if (so != 0) {
+        const bool direct = so == sgn;
+        mp_g = (direct ? A.cand : A.vcand) + d0;
+        vp_g = (direct ? A.vcand : A.cand) + d0;
+        const int c0 = A.scan_cnt[((int64_t)f * NW + wid) * 2], c1 = A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1];
+        cm = direct ? c0 : c1;
+        cv = direct ? c1 : c0;
     } else {
-    /* one coalesced load per 64 positions, issued a block ahead; the left and
-     * right neighbours come from the adjacent lanes (DPP wave shifts), the
-     * block edges from the previous / next block's end lanes */
-    double xc = w0 < w1 && w0 + lane < n ? sg * e[w0 + lane] : 0.0;
-    double xedge = w0 < w1 ? sg * e[w0 - 1] : 0.0;           /* position b - 1 */
-    for (int64_t b = w0; b < w1; b += 64) {
-        const int64_t i = b + lane;
-        const double xn = b + 64 + lane < n ? sg * e[b + 64 + lane] : 0.0;
-        const double xl = dpp_shr1_d(xc, xedge);
-        const double xr1 = dpp_shl1_d(xc, __shfl(xn, 0));
-        bool ism = false, isv = false;
-        int32_t pk = 0;
-        if (i < w1) {
-            const double xi = xc;
-            if (xl != xi) {
-                int64_t ia = i + 1;
-                double xr = xr1;
-                if (xr == xi && ia < n - 1) {                    /* plateau: walk it */
-                    ia = i + 2;
-                    while (ia < n - 1 && sg * e[ia] == xi) ia++;
-                    xr = sg * e[ia];
-                }
-                /* a valley's plateau midpoint too (its value is the plateau's):
-                 * the other sign's launch takes it as a maximum */
-                if (xl < xi && xr < xi) { ism = true; pk = (int32_t)((i + ia - 1) >> 1); }
-                else if (xl > xi && xr > xi) { isv = true; pk = (int32_t)((i + ia - 1) >> 1); }
-            }
+        mp_g = A.cand + d0;
+        vp_g = A.vcand + d0;
+        fp_scan_wave([&](int64_t i) { return sg * e[i]; }, n, w0, w1, mp_g, vp_g, cm, cv);
+        if (A.scan_ok && lane == 0) {
+            A.scan_cnt[((int64_t)f * NW + wid) * 2] = cm;
+            A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1] = cv;
         }
-        const unsigned long long bm = __ballot(ism), bv = __ballot(isv);
-        if (ism) mp_g[w0 - 1 + cm + __popcll(bm & lt)] = pk;
-        if (isv) vp_g[w0 - 1 + cv + __popcll(bv & lt)] = pk;
-        cm += __popcll(bm);
-        cv += __popcll(bv);
-        xedge = __shfl(xc, 63);
-        xc = xn;
-    }
-    if (record && lane == 0) {
-        A.scan_cnt[((int64_t)f * NW + wid) * 2] = cm;
-        A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1] = cv;
-    }
     }
     if (lane == 0) { s_gc[0][0][wid] = cm; s_gc[1][0][wid] = cv; }
     __syncthreads();
@@ -717,13 +681,13 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     if (M > FL_MC) {                                         /* k_find_peaks takes this recording */
         if (tid == 0) {
             A.fallback[f] = 1;
-            if (record) A.scan_ok[f] = 0;
+            if (A.scan_ok) A.scan_ok[f] = 0;                 /* (it rewrites cand) */
         }
         return;
     }
     if (tid == 0) {
         A.fallback[f] = 0;
-        if (record) A.scan_ok[f] = 1;
+        if (A.scan_ok && so == 0) A.scan_ok[f] = sgn;
     }
     const int64_t dist = A.distance;
     for (int t = lane; t < cm; t += 64) {                    /* this wave's run of maxima */
