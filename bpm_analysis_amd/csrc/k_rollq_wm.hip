@@ -461,6 +461,13 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     uint16_t *posB = posA + m8;
     uint32_t *kh = (uint32_t *)(posB + m8);
     uint32_t *cnt = kh + m8;
+    /* per-wave digit bins for the peer masks (lanes with this lane's digit):
+     * each valid lane ORs its bit into its digit's bin and reads the bin back
+     * (three LDS instructions instead of eight ballots and ~48 VALU per item);
+     * past the counters while they fit, else match8 */
+    const size_t wbin_off = (size_t)8 * m8 + (size_t)NWV * 128 * 4;
+    unsigned long long *wbin_all =
+        wbin_off + (size_t)NWV * 256 * 8 <= Lay.total - Lay.area ? (unsigned long long *)(smem + Lay.area + wbin_off) : nullptr;
 
     /* ---------------- 1. ranks by LSD radix sort ----------------
      * Keys: the order-preserving 64-bit key minus the curve's lowest key,
@@ -501,6 +508,8 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             kand &= (uint64_t)__shfl_xor((long long)kand, o);
         }
         if (lane == 0) { s_or[wid] = kor; s_and[wid] = kand; }
+        if (wbin_all)
+            for (int j = tid; j < NWV * 256; j += WM_T) wbin_all[j] = 0ull;
         __syncthreads();
         uint64_t vary = 0;
         {
@@ -533,12 +542,23 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                     const int slot = wid * S + i * 64 + lane;
                     const bool valid = slot < m;
                     const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                    const uint64_t peers = match8(dg) & __ballot(valid);
+                    uint64_t peers;
+                    if (wbin_all) {                          /* uniform */
+                        unsigned long long *bin = wbin_all + wid * 256 + dg;
+                        if (valid) atomicOr(bin, 1ull << lane);
+                        peers = __hip_atomic_load(bin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        peers = match8(dg);
+                    }
+                    peers &= __ballot(valid);
                     const uint64_t below = peers & lanemask_lt();
                     const int leader = valid ? __ffsll((long long)peers) - 1 : lane;
                     uint32_t base = 0;
-                    if (valid && below == 0)   /* LDS atomics of one wave land in issue (= slot) order */
+                    if (valid && below == 0) {   /* LDS atomics of one wave land in issue (= slot) order */
                         base = atomicAdd(&wc[dg >> 1], (uint32_t)__popcll(peers) << (16 * (dg & 1)));
+                        if (wbin_all) __hip_atomic_store(wbin_all + wid * 256 + dg, 0ull, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);   /* after every peer's read */
+                    }
                     base = (uint32_t)__shfl((int)base, leader);
                     const uint32_t rnk = ((base >> (16 * (dg & 1))) & 0xFFFFu) + (uint32_t)__popcll(below);
                     if ((i & 1) == 0) rk16[i >> 1] = rnk; else rk16[i >> 1] |= rnk << 16;
