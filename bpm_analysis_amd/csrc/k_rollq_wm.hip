@@ -183,16 +183,17 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             const int64_t *trg = A.troughs + d0;
             return interp_at(x, trg, [&](int j) { return A.env[d0 + trg[j]]; }, ntr_all);
         }
-        if (ntr == 0 || x < s_tp[0]) return __builtin_nan("");
-        int j = s_bj[(x - xb) >> 6];
+        const int xi = (int)x;                               /* positions < 2^31 (host check): 32-bit arithmetic */
+        if (ntr == 0 || xi < s_tp[0]) return __builtin_nan("");
+        int j = s_bj[(xi - (int)xb) >> 6];
         if (j < 0) j = 0;
-        while (j + 1 < ntr && s_tp[j + 1] <= x) ++j;
-        if (j == ntr - 1 || s_tp[j] == x) return s_tv[j];
+        while (j + 1 < ntr && s_tp[j + 1] <= xi) ++j;
+        if (j == ntr - 1 || s_tp[j] == xi) return s_tv[j];
         const double y0 = s_tv[j], y1 = s_tv[j + 1];
         const double slope = PRUNE ? s_sl[j] : (y1 - y0) / ((double)s_tp[j + 1] - (double)s_tp[j]);
-        double r = slope * ((double)x - (double)s_tp[j]) + y0;
+        double r = slope * ((double)xi - (double)s_tp[j]) + y0;
         if (r != r) {
-            r = slope * ((double)x - (double)s_tp[j + 1]) + y1;
+            r = slope * ((double)xi - (double)s_tp[j + 1]) + y1;
             if (r != r && y0 == y1) r = y0;
         }
         return r;
@@ -679,7 +680,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
         for (int bk = b0; bk < b1; ++bk) {
             const int i0 = (int)o0 + (bk << 6), i = i0 + lane;
             bool valid = false;
-            int plo = 0, phi = 0, t = 0, nobs = 0;
+            int plo = 0, phi = 0, t = 0, nobs = 0, kq = 0;
+            double idxq = 0.0;                               /* pandas' quantile index and its interpolation */
+            bool intq = false;
             if (i < (int)o1) {
                 const int ee = i + 1 + off, ss = ee - Wi;
                 const int e = ee < ni ? ee : ni, sc = ss > 0 ? ss : 0;
@@ -690,9 +693,8 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                     plo = kidx(lo - t0i);
                     phi = kidx(e - t0i);
                     const int lw = PRUNE ? lidx(e - t0i) - lidx(lo - t0i) : 0;
-                    double idxf;
-                    bool interp;
-                    t = target(nobs, idxf, interp) - lw;
+                    kq = target(nobs, idxq, intq);
+                    t = kq - lw;
                 }
             }
             const uint64_t vm0 = __ballot(valid);
@@ -854,9 +856,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
                 ia = ia < need ? ia : need - 1;                  /* (never binds; keeps a corrupted walk in bounds) */
                 ib = ib < need ? ib : need - 1;
                 if (valid) {
-                    double idxf;
-                    bool interp;
-                    const int k = target(nobs, idxf, interp);
+                    const int k = kq;
+                    const double idxf = idxq;
+                    const bool interp = intq;
                     const double va = svl ? svl[wl[ia]] : dval(t0 + spos(posR[wl[ia]]));
                     if (!interp) {
                         res = va;
