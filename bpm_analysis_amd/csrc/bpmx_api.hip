@@ -809,7 +809,12 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.vfl = draft_vfl;
             a.nund = draft_vfl + 2 * F;                        /* zeroed by k_init_out */
             LAUNCH(ctx, s, "k_draft_bounds", k_draft_bounds, dim3(F, gy), dim3(DB_T), 0, s, a);
-            const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8, (trmax + DP_CHUNK - 1) / DP_CHUNK));
+            /* at most BPMX_DP_GY workgroups per recording, each taking every
+             * gridDim.y-th chunk of 32 troughs */
+#ifndef BPMX_DP_GY
+#define BPMX_DP_GY 4
+#endif
+            const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>(BPMX_DP_GY, (trmax + DP_CHUNK - 1) / DP_CHUNK));
             LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
             LAUNCH(ctx, s, "k_draft_points[wide]", k_draft_points<4>, dim3(F, gp), dim3(DB_T), 0, s, a);
         }
@@ -827,7 +832,14 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             FinalArgs a;
             a.draft = draft; a.doff = d_doff; a.active = d_active; a.qv = qv; a.allnan_draft = d_an1;
             a.allnan_final = d_an2; a.n_files = F; a.floor = O->floor; a.flags = O->flags;
-            LAUNCH(ctx, s, "k_floor_final", k_floor_final, g2, dim3(256), 0, s, a);
+            /* one workgroup per recording unless they are long: most recordings
+             * exit at once, and a static or draft floor is a short fill */
+#ifndef BPMX_FF_WIDE
+            const dim3 gf(maxnd > 65536 ? g2.x : 1u, (unsigned)F);
+#else
+            const dim3 gf = g2;
+#endif
+            LAUNCH(ctx, s, "k_floor_final", k_floor_final, gf, dim3(256), 0, s, a);
         }
     }
 
