@@ -78,7 +78,7 @@ def parse(argv=None):
                          "stream's; a fourth stream shares one and serialises)")
     ap.add_argument("--c5-parity-files", type=int, default=-1,
                     help="C5: each rank's shortest recordings checked against the oracle (-1: every recording of "
-                         "the rank; ~15 s of 16-thread oracle time per 64 recordings)"),
+                         "the rank; ~15 s of 16-thread oracle time per 64 recordings)")
     ap.add_argument("--dropin-files", type=int, default=3,
                     help="side measurement: per-file latency of the reference's call sequence through the "
                          "drop-in on 60 s WAV files (0: skip)")

@@ -14,13 +14,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # BPMX_LIB: another build of the same library (diagnostic A/B runs of kernel variants)
 LIB_PATH = os.environ.get("BPMX_LIB") or os.path.join(_HERE, "libbpmx.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DT_U8, DT_I16, DT_I32, DT_F32, DT_F64 = 0, 1, 2, 3, 4
 MODE_REFERENCE, MODE_NATIVE = 0, 1
 STAGE_ENVELOPE, STAGE_FLOOR, STAGE_PEAKS, STAGE_ALL = 1, 2, 4, 7
 F_STATIC_FLOOR, F_DRAFT_FLOOR, F_NAN_FLOOR, F_TOO_SHORT, F_BAD_WINDOW = 1, 2, 4, 8, 16
 F_TROUGH_TIE, F_PEAK_TIE = 32, 64      # decisive height tie in find_peaks' distance filter (bpmx.h)
+F_TROUGH_ORDERED, F_PEAK_ORDERED = 128, 256   # that filter ran in the caller's np.argsort order (bpmx_run_ordered)
 OPT_ROLLQ_MERGE = 1
 OPT_NATIVE_F64 = 2
 OPT_HILBERT_ROCFFT = 4
@@ -39,7 +40,7 @@ STAT_RAW_TROUGHS, STAT_UNDECIDED, STAT_FULL_DRAFT, NSTATS = 0, 1, 2, 8
 OK, E_ARG, E_HIP, E_LIMIT, E_NODEV = 0, -1, -2, -3, -4
 
 EXPORTS = ["bpmx_abi_version", "bpmx_last_error", "bpmx_create", "bpmx_destroy", "bpmx_decimated_length",
-           "bpmx_run", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only",
+           "bpmx_run", "bpmx_run_ordered", "bpmx_synth", "bpmx_synth_host", "bpmx_profile", "bpmx_profile_read", "bpmx_profile_only",
            "bpmx_stats", "bpmx_set_pipeline"]
 
 
@@ -64,6 +65,13 @@ class Out(ctypes.Structure):
     _fields_ = [("env", ctypes.c_void_p), ("floor", ctypes.c_void_p), ("y", ctypes.c_void_p),
                 ("troughs", ctypes.c_void_p), ("peaks", ctypes.c_void_p), ("n_troughs", ctypes.c_void_p),
                 ("n_peaks", ctypes.c_void_p), ("flags", ctypes.c_void_p), ("n_raw_troughs", ctypes.c_void_p)]
+
+
+class PeakOrder(ctypes.Structure):
+    """bpmx_peak_order: per search (0 = troughs, 1 = raw peaks) the candidate
+    export and the caller's visiting ranks (device pointers or None)."""
+    _fields_ = [("cand", ctypes.c_void_p * 2), ("n_cand", ctypes.c_void_p * 2),
+                ("rank", ctypes.c_void_p * 2), ("use_rank", ctypes.c_void_p * 2)]
 
 
 class BpmxError(RuntimeError):
@@ -110,6 +118,9 @@ def load() -> ctypes.CDLL:
     L.bpmx_decimated_length.restype = I64
     L.bpmx_run.argtypes = [P, ctypes.POINTER(Params), ctypes.POINTER(Batch), ctypes.POINTER(Out), P]
     L.bpmx_run.restype = ctypes.c_int
+    L.bpmx_run_ordered.argtypes = [P, ctypes.POINTER(Params), ctypes.POINTER(Batch), ctypes.POINTER(Out),
+                                   ctypes.POINTER(PeakOrder), P]
+    L.bpmx_run_ordered.restype = ctypes.c_int
     L.bpmx_synth.argtypes = [P, U64, I32, ctypes.POINTER(ctypes.c_int64), I32, I32, P, P]
     L.bpmx_synth.restype = ctypes.c_int
     L.bpmx_synth_host.argtypes = [U64, I64, I32, I32, P]

@@ -253,19 +253,24 @@ int bpmx_stats(bpmx_ctx *ctx, int64_t *out, int n) {
     return BPMX_NSTATS;
 }
 
-/* the rolling-quantile kernels' dynamic-LDS limit, raised once per process
- * to the largest layout they take (not per launch on the run path) */
-static void wm_lds_attr() {
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const int mx = (int)wm_layout(WM_MMAX, false).total;
-        (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    });
+/* the rolling-quantile kernels' dynamic-LDS limit, raised once per device
+ * (the attribute applies to the current device) to the largest layout they
+ * take, not per launch on the run path */
+static void wm_lds_attr(int device) {
+    static std::mutex mu;
+    static std::vector<char> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0) return;
+    if ((int)done.size() <= device) done.resize((size_t)device + 1, 0);
+    if (done[(size_t)device]) return;
+    const int mx = (int)wm_layout(WM_MMAX, false).total;
+    (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    done[(size_t)device] = 1;
 }
 
 static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream,
-                    bool env_active) {
+                    bool env_active, const bpmx_peak_order *ord = nullptr) {
     if (!ctx || !P || !B || !O) return fail(BPMX_E_ARG, "NULL argument");
     const int F = B->n_files;
     if (F < 1 || !B->frame_offsets) return fail(BPMX_E_ARG, "empty batch");
@@ -544,7 +549,17 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     bs.env = O->env; bs.doff = d_doff; bs.boff = d_boff; bs.active = d_active; bs.n_files = F;
     bs.bmax = bmax; bs.bmin = bmin; bs.skip_le = QR_MAX;     /* k_quantile_reg writes those tables */
     const bool long_files = maxnd > QR_MAX;
-    const bool fp_global = (P->options & BPMX_OPT_PEAKS_GLOBAL) != 0;
+    /* an ordered run (bpmx_run_ordered: candidate export, the caller's visiting
+     * ranks) takes k_find_peaks, the kernel that implements them */
+    const bool fp_global = (P->options & BPMX_OPT_PEAKS_GLOBAL) != 0 || ord != nullptr;
+    auto set_order = [&](PeakArgs &a, int search) {
+        if (!ord) return;
+        a.cand_out = ord->cand[search];
+        a.ncand_out = ord->n_cand[search];
+        a.rank = ord->rank[search];
+        a.use_rank = ord->use_rank[search];
+        a.ordered_bit = search == 0 ? BPMX_F_TROUGH_ORDERED : BPMX_F_PEAK_ORDERED;
+    };
     /* find_peaks: k_find_peaks_lds for every recording it holds; the others
      * (longer than FPL_NMIN, or more than FL_MC maxima) take the multi-
      * workgroup k_fpl_* path when the batch has long recordings, else the
@@ -647,6 +662,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5; a.tie_bit = BPMX_F_TROUGH_TIE;
             a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;
+            set_order(a, 0);
             FIND_PEAKS(a, "troughs");
         }
         if (bad_window)
@@ -737,7 +753,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                  * kept samples, > WM_TRMAX troughs, a compact-key collision)
                  * runs unpruned in the same workgroup, so its LDS is the
                  * larger layout (BPMX_OPT_ROLLQ_NOPRUNE: unpruned for all) */
-                wm_lds_attr();
+                wm_lds_attr(ctx->device);
                 if (!(P->options & BPMX_OPT_ROLLQ_NOPRUNE))
                     LAUNCH(ctx, s, "k_rollq_wm", k_rollq_wm_t<true>, dim3(F, (unsigned)wm_nch), dim3(WM_T),
                            std::max(wm_lds_p, wm_lds), s, a, wm_pos, wm_full);
@@ -850,7 +866,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;
         a.sign = 1.0; a.cand = cand; a.state = state; a.out = O->peaks; a.nout = O->n_peaks;
         a.run_out = nullptr; a.run_min = 0; a.tie_bit = BPMX_F_PEAK_TIE;
-        a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;   /* the run's scan record: Hilbert's or the trough launch's */
+        a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;   /* the run's scan record: the trough launch's */
+        set_order(a, 1);
         FIND_PEAKS(a, "peaks");
     }
 #undef FIND_PEAKS
@@ -1004,6 +1021,19 @@ int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus) {
     ctx->pipe_env_cus = env_cus;
     ctx->pipe_det_cus = det_cus;
     return BPMX_OK;
+}
+
+int bpmx_run_ordered(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O,
+                     const bpmx_peak_order *order, void *stream) {
+    if (!order) return bpmx_run(ctx, P, B, O, stream);
+    for (int s = 0; s < 2; ++s) {
+        if ((order->cand[s] != nullptr) != (order->n_cand[s] != nullptr))
+            return fail(BPMX_E_ARG, "bpmx_peak_order: cand and n_cand go together");
+        if ((order->rank[s] != nullptr) != (order->use_rank[s] != nullptr))
+            return fail(BPMX_E_ARG, "bpmx_peak_order: rank and use_rank go together");
+    }
+    if (P && (P->options & BPMX_OPT_STATS)) return fail(BPMX_E_ARG, "bpmx_run_ordered: no BPMX_OPT_STATS");
+    return run_impl(ctx, P, B, O, stream, false, order);
 }
 
 int bpmx_run(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, void *stream) {

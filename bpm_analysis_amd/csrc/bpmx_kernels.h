@@ -122,11 +122,18 @@ struct PeakArgs {
     int32_t *flags;        /* [F] per-file flags: tie_bit is OR'd in when the distance filter met a decisive tie */
     int32_t tie_bit;       /* BPMX_F_TROUGH_TIE or BPMX_F_PEAK_TIE */
     /* the run's extrema scan record (bpmx_fpscan.h): ok[f] = +1 / -1 when
-     * k_hilbert_env or an earlier find_peaks launch of this run left the
-     * lists in cand / vcand (made for x = +env / -env), 0 = scan here (and
-     * record); null: no record */
+     * the trough launch of k_find_peaks_lds (the only writer) left the lists
+     * in cand / vcand (made for x = +env / -env), 0 = scan here (and record);
+     * null: no record */
     int32_t *scan_ok = nullptr;    /* [F] */
     int32_t *scan_cnt = nullptr;   /* [F][FPS_NW][2] */
+    /* bpmx_run_ordered (k_find_peaks only): candidate export and the caller's
+     * visiting ranks (include/bpmx.h bpmx_peak_order) */
+    int32_t *cand_out = nullptr;   /* [sumNd] or null */
+    int32_t *ncand_out = nullptr;  /* [F] */
+    const int32_t *rank = nullptr; /* [sumNd] or null */
+    const int32_t *use_rank = nullptr;  /* [F] */
+    int32_t ordered_bit = 0;       /* BPMX_F_TROUGH_ORDERED or BPMX_F_PEAK_ORDERED */
 #ifdef BPMX_STAMPS
     unsigned long long *stamps;
 #endif

@@ -443,6 +443,13 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
         m += s_flag;
         __syncthreads();
     }
+    if (A.cand_out) {                                        /* bpmx_run_ordered: the candidate list */
+        for (int j = tid; j < m; j += FP_T) A.cand_out[d0 + j] = cp_g[j];
+        if (tid == 0) A.ncand_out[f] = m;
+    }
+    /* the caller's visiting ranks (np.argsort of the heights): they decide the
+     * distance filter alone; without them the stable order below */
+    const int32_t *rk = (A.rank && A.use_rank && A.use_rank[f]) ? A.rank + d0 : nullptr;
     const bool lds = m <= FP_MC;
     int32_t *cp = lds ? s_cp : cp_g;
     uint8_t *st = lds ? s_st : A.state + d0;
@@ -473,9 +480,10 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
                 if (ld_state(&st[j]) != ST_UNDECIDED) continue;
                 const int64_t pj = cp[j];
                 const double vj = cval(j);
+                const int32_t rj = rk ? rk[j] : 0;
                 bool killed = false, blocked = false;
                 for (int k = j - 1; k >= 0 && pj - cp[k] < dist; --k) {
-                    if (cval(k) > vj) {                  /* earlier index wins only when strictly higher */
+                    if (rk ? rk[k] > rj : cval(k) > vj) { /* earlier index wins only when strictly higher */
                         const uint8_t s = ld_state(&st[k]);
                         if (s == ST_KEPT) { killed = true; break; }
                         if (s == ST_UNDECIDED) blocked = true;
@@ -483,7 +491,7 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
                 }
                 if (!killed) {
                     for (int k = j + 1; k < m && cp[k] - pj < dist; ++k) {
-                        if (cval(k) >= vj) {             /* later index wins ties (stable argsort order) */
+                        if (rk ? rk[k] > rj : cval(k) >= vj) {  /* later index wins ties (stable argsort order) */
                             const uint8_t s = ld_state(&st[k]);
                             if (s == ST_KEPT) { killed = true; break; }
                             if (s == ST_UNDECIDED) blocked = true;
@@ -504,8 +512,9 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
 
     STAMP(2);
     /* decisive tie (include/bpmx.h BPMX_F_*_TIE): a removed candidate with no
-     * strictly higher kept candidate within dist was removed by an equal one */
-    if (dist > 1) {
+     * strictly higher kept candidate within dist was removed by an equal one
+     * (none with the caller's ranks: the order is then the reference's) */
+    if (dist > 1 && !rk) {
         for (int j = tid; j < m; j += FP_T) {
             if (ld_state(&st[j]) != ST_REMOVED) continue;
             const int64_t pj = cp[j];
@@ -579,7 +588,10 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
     if (tid == 0) {
         A.nout[f] = w;
         if (A.run_out) A.run_out[f] = w >= A.run_min ? 1 : 0;
-        if (s_tie && A.flags) A.flags[f] |= A.tie_bit;
+        if (A.flags) {
+            if (rk) A.flags[f] |= A.ordered_bit;
+            else if (s_tie) A.flags[f] |= A.tie_bit;
+        }
     }
     STAMP(4);
     STAMP_FLUSH(A.stamps);
@@ -646,9 +658,9 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
      * no workgroup barrier), compacting its hits into its own stretch of the
      * global scratch (a run of c positions holds at most c hits); one scan of
      * the 16 per-wave counts then places every run (bpmx_fpscan.h).  When this
-     * run's scan record holds the lists (k_hilbert_env, or the trough launch
-     * for the peak launch) they are taken as they are, swapped for the other
-     * sign: -env's maxima are env's valleys and its valleys env's maxima. */
+     * run's scan record holds the lists (written only by the trough launch,
+     * read by the peak launch) they are taken as they are, swapped for the
+     * other sign: -env's maxima are env's valleys and its valleys env's maxima. */
     static_assert(NW == FPS_NW, "the scan record's per-wave runs");
     int64_t w0, w1;
     fp_scan_run(n, wid, w0, w1);

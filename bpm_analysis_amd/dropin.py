@@ -52,13 +52,23 @@ def _file_error(flags: int, params: Dict, sr: int):
 TIE_MSG = ("find_peaks' distance filter met equal-height {what} closer than `distance`: numpy's argsort order "
            "for equal heights is implementation-defined, so these {what} may differ from the reference's on "
            "this machine (bpmx keeps the later index).")
+ORDERED_MSG = ("find_peaks' distance filter met equal-height {what} closer than `distance`; decided in numpy's "
+               "argsort order, as the reference's own call does on this machine.")
 
 
 def _warn_ties(flags: int, what: str) -> None:
-    """Report a decisive tie (include/bpmx.h BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE)."""
-    bit = N.F_TROUGH_TIE if what == "troughs" else N.F_PEAK_TIE
-    if flags & bit:
+    """Report a decisive tie (include/bpmx.h BPMX_F_TROUGH_TIE / BPMX_F_PEAK_TIE).
+
+    The drop-in entry points run with ``resolve_ties`` (engine.Detector.resolve_ties),
+    so a flagged recording has been re-decided in numpy's order and carries
+    F_*_ORDERED instead (a debug line); the warning is left for a result that
+    still holds the library's stable order."""
+    tie = N.F_TROUGH_TIE if what == "troughs" else N.F_PEAK_TIE
+    ordered = N.F_TROUGH_ORDERED if what == "troughs" else N.F_PEAK_ORDERED
+    if flags & tie:
         logging.warning(TIE_MSG.format(what=what))
+    elif flags & ordered:
+        logging.debug(ORDERED_MSG.format(what=what))
 
 
 def _read_wav(file_path: str):
@@ -133,7 +143,8 @@ def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: 
     stages = N.STAGE_ALL if d.distance >= 1 else N.STAGE_ENVELOPE     # distance < 1 raises in the later calls
     det = default_detector(device)
     try:
-        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file))[0]
+        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file),
+                         resolve_ties=True)[0]
     except N.BpmxError as exc:
         if stages == N.STAGE_ENVELOPE or not exc.per_file:
             raise
@@ -141,7 +152,8 @@ def preprocess_audio(file_path: str, params: Dict, output_directory: str, mode: 
         # envelope alone now, so the error surfaces from the floor call as in
         # the reference (:1732), after the debug WAV is written
         stages = N.STAGE_ENVELOPE
-        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file))[0]
+        r = det.run_host([audio], sample_rate, params, mode=mode, stages=stages, want_y=bool(save_debug_file),
+                         resolve_ties=True)[0]
     if save_debug_file:
         _write_debug_wav(f"{os.path.splitext(file_path)[0]}_filtered_debug.wav", d.sr, r["y"])
         base = os.path.basename(os.path.splitext(file_path)[0])
@@ -166,7 +178,7 @@ def _calculate_dynamic_noise_floor(audio_envelope: np.ndarray, sample_rate: int,
         raise ValueError(DISTANCE_MSG)
     r = _cached(env, sample_rate, "floor_key", _floor_key(params, sample_rate))
     if r is None:
-        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_FLOOR)[0]
+        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_FLOOR, resolve_ties=True)[0]
     fl = r["flags"]
     if fl & N.F_BAD_WINDOW:
         raise _window_error(params, sample_rate)
@@ -190,7 +202,8 @@ def find_raw_peaks(audio_envelope: np.ndarray, sample_rate: int, params: Dict, h
     floor = np.ascontiguousarray(np.broadcast_to(np.asarray(height_threshold, dtype=np.float64), env.shape))
     r = _cached(env, sample_rate, "peak_key", _peak_key(params, sample_rate))
     if r is None or not _same_bytes(r["floor"], floor):
-        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor])[0]
+        r = default_detector(device).run_env_host([env], sample_rate, params, N.STAGE_PEAKS, floors=[floor],
+                                                  resolve_ties=True)[0]
     peaks = np.array(r["peaks"], dtype=np.int64)
     _warn_ties(r["flags"], "peaks")
     logging.info(f"Found {len(peaks)} raw peaks using dynamic height threshold.")
@@ -211,7 +224,8 @@ def analyze_batch(recordings: Sequence[np.ndarray], fs: int, params: Dict, mode:
     ``flags & F_TOO_SHORT`` and no outputs instead of failing the batch.
     """
     design(fs, params)   # Nyquist check / clamp warnings once per batch
-    return default_detector(device).run_host(list(recordings), fs, params, mode=mode, stages=N.STAGE_ALL)
+    return default_detector(device).run_host(list(recordings), fs, params, mode=mode, stages=N.STAGE_ALL,
+                                             resolve_ties=True)
 
 
 def analyze_wav_files(file_paths: Sequence[str], params: Dict, output_directory: str, mode: str = None,
@@ -255,7 +269,8 @@ def analyze_wav_files(file_paths: Sequence[str], params: Dict, output_directory:
         try:
             if d.distance < 1:
                 raise ValueError(DISTANCE_MSG)
-            res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save)
+            res = det.run_host([audio[k][1] for k in idx], fs, params, mode=mode, stages=N.STAGE_ALL, want_y=save,
+                               resolve_ties=True)
         except (ValueError, N.BpmxError) as exc:      # reported per file, as the GUI loop does (gui.py:247-251)
             if isinstance(exc, N.BpmxError) and not exc.per_file:
                 raise                                 # HIP / device failure: not a per-file error

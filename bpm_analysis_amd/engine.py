@@ -153,9 +153,12 @@ class Detector:
 
     def run(self, pcm, frame_offsets: Sequence[int], fs: int, params: dict, mode: str = "reference",
             stages: int = N.STAGE_ALL, channels: int = 1, out: Optional[Result] = None, want_y: bool = False,
-            d: Optional[Design] = None, log: bool = False, options: int = 0) -> Result:
+            d: Optional[Design] = None, log: bool = False, options: int = 0,
+            order: Optional[N.PeakOrder] = None) -> Result:
         """Run `stages` over a device batch.  `pcm` is a CUDA tensor (or None when
-        ENVELOPE is not requested and `out.env` already holds the envelopes)."""
+        ENVELOPE is not requested and `out.env` already holds the envelopes).
+        `order`: bpmx_run_ordered's candidate export / visiting ranks (see
+        ``resolve_ties``)."""
         if d is None:
             d = design(fs, params, log=log)
         fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
@@ -182,9 +185,103 @@ class Detector:
         o.n_troughs, o.n_peaks, o.flags = ptr(out.n_troughs), ptr(out.n_peaks), ptr(out.flags)
         o.n_raw_troughs = ptr(out.n_raw_troughs)
         with self.lock:
-            N.check(self.L.bpmx_run(self.ctx, ctypes.byref(p), ctypes.byref(b), ctypes.byref(o),
-                                    self.stream_handle()), "bpmx_run")
+            if order is None:
+                N.check(self.L.bpmx_run(self.ctx, ctypes.byref(p), ctypes.byref(b), ctypes.byref(o),
+                                        self.stream_handle()), "bpmx_run")
+            else:
+                N.check(self.L.bpmx_run_ordered(self.ctx, ctypes.byref(p), ctypes.byref(b), ctypes.byref(o),
+                                                ctypes.byref(order), self.stream_handle()), "bpmx_run_ordered")
         return out
+
+    def resolve_ties(self, out: Result, params: dict, stages: int = N.STAGE_ALL) -> int:
+        """Re-decide find_peaks' distance filter in numpy's own argsort order for
+        the recordings of `out` that carry a decisive-tie bit (F_TROUGH_TIE /
+        F_PEAK_TIE), so their troughs, floor and raw peaks are the reference's
+        on this machine.
+
+        scipy visits the distance filter's candidates in ``np.argsort(x[peaks])``
+        order (``_select_by_peak_distance``, scipy/signal/_peak_finding.py:976-980,
+        called from bpm_analysis.py:1070 and :227).  Among equal heights that
+        order is numpy's implementation detail, so it is computed here, by numpy,
+        from the candidate list the library exports; the library then decides the
+        filter by those ranks (include/bpmx.h ``bpmx_run_ordered``).  Troughs
+        first: a new trough set changes the floor and so the peak search's
+        candidates, whose order is taken after.  The flagged recordings run as a
+        sub-batch (ds = 1, envelopes gathered on the device); their results are
+        written back into `out` and their flags carry F_*_ORDERED instead of
+        F_*_TIE.  Returns the number of recordings re-run (0: nothing to do, no
+        launch).  Synchronises the current stream."""
+        torch = _torch()
+        det_st = stages & (N.STAGE_FLOOR | N.STAGE_PEAKS)
+        bits = (N.F_TROUGH_TIE if det_st & N.STAGE_FLOOR else 0) | (N.F_PEAK_TIE if det_st & N.STAGE_PEAKS else 0)
+        if not bits:
+            return 0
+        flags = out.flags.cpu().numpy()
+        sel = np.flatnonzero(flags & bits)
+        if sel.size == 0:
+            return 0
+        F = int(sel.size)
+        lens = out.doff[sel + 1] - out.doff[sel]
+        fo = np.zeros(F + 1, dtype=np.int64)
+        fo[1:] = np.cumsum(lens)
+        tot = int(fo[-1])
+        d = detect_design(out.sr, params)
+        dev = self.device
+        idx = torch.from_numpy(np.concatenate([np.arange(out.doff[f], out.doff[f + 1]) for f in sel])).to(dev)
+        sub = self.alloc(fo, 1, d.sr)
+        sub.env.copy_(out.env[idx])
+        if not det_st & N.STAGE_FLOOR:
+            sub.floor.copy_(out.floor[idx])
+        env_h = sub.env.cpu().numpy()
+        i32 = lambda k: torch.zeros(max(k, 1), dtype=torch.int32, device=dev)
+        cand, ncand = [i32(tot), i32(tot)], [i32(F), i32(F)]
+        rank, use = [i32(tot), i32(tot)], [i32(F), i32(F)]
+
+        def order(export, ranked):
+            o = N.PeakOrder()
+            for s in export:
+                o.cand[s], o.n_cand[s] = cand[s].data_ptr(), ncand[s].data_ptr()
+            for s in ranked:
+                o.rank[s], o.use_rank[s] = rank[s].data_ptr(), use[s].data_ptr()
+            return o
+
+        def set_ranks(s, files, sign):
+            c, nc = cand[s].cpu().numpy(), ncand[s].cpu().numpy()
+            r, u = np.zeros(max(tot, 1), dtype=np.int32), np.zeros(F, dtype=np.int32)
+            for k in files:
+                a, m = int(fo[k]), int(nc[k])
+                x = env_h[a:int(fo[k + 1])]
+                x = -x if sign < 0 else x                     # find_peaks(-env) negates the array (:1070)
+                perm = np.argsort(x[c[a:a + m]])              # the call _select_by_peak_distance makes
+                r[a + perm] = np.arange(m, dtype=np.int32)
+                u[k] = 1
+            rank[s].copy_(torch.from_numpy(r))
+            use[s].copy_(torch.from_numpy(u))
+
+        run = lambda st, o: self.run(None, fo, d.sr, params, stages=st, out=sub, d=d, order=o)
+        ranked = set()
+        if det_st & N.STAGE_FLOOR and (flags[sel] & N.F_TROUGH_TIE).any():
+            run(det_st, order({0}, ()))
+            set_ranks(0, np.flatnonzero(flags[sel] & N.F_TROUGH_TIE), -1.0)
+            ranked.add(0)
+        run(det_st, order({1} if det_st & N.STAGE_PEAKS else (), ranked))
+        fl = sub.flags.cpu().numpy().copy()
+        if det_st & N.STAGE_PEAKS and (fl & N.F_PEAK_TIE).any():
+            p2 = np.flatnonzero(fl & N.F_PEAK_TIE)
+            set_ranks(1, p2, 1.0)
+            run(N.STAGE_PEAKS, order((), {1}))
+            pb = N.F_PEAK_TIE | N.F_PEAK_ORDERED
+            fl = (fl & ~pb) | (sub.flags.cpu().numpy() & pb)
+        if det_st & N.STAGE_FLOOR:
+            out.floor[idx] = sub.floor[:tot]
+            out.troughs[idx] = sub.troughs[:tot]
+            out.n_troughs[sel] = sub.n_troughs
+            out.n_raw_troughs[sel] = sub.n_raw_troughs
+        if det_st & N.STAGE_PEAKS:
+            out.peaks[idx] = sub.peaks[:tot]
+            out.n_peaks[sel] = sub.n_peaks
+        out.flags[torch.from_numpy(sel).to(dev)] = torch.from_numpy(fl).to(dev)
+        return F
 
     def synth(self, frame_offsets: Sequence[int], fs: int, channels: int = 1, seed0: int = 0,
               seeds: Optional[Sequence[int]] = None):
@@ -236,12 +333,14 @@ class Detector:
     # ------------------------------------------------------------------ #
     def run_host(self, recordings: List[np.ndarray], fs: int, params: dict, mode: str = "reference",
                  stages: int = N.STAGE_ALL, want_y: bool = False, log: bool = False,
-                 options: int = 0, longest_first: bool = True) -> List[dict]:
+                 options: int = 0, longest_first: bool = True, resolve_ties: bool = False) -> List[dict]:
         """Host arrays in, per-file host results out (H2D + run + D2H).
 
         A ragged batch runs longest recording first (shard.longest_first: LPT
         over the CUs, since recording f is workgroup f of every per-recording
-        kernel); results come back in the caller's order."""
+        kernel); results come back in the caller's order.  `resolve_ties`:
+        decisive find_peaks ties re-decided in numpy's order (``resolve_ties``;
+        the drop-in entry points set it)."""
         torch = _torch()
         if not recordings:
             return []
@@ -249,7 +348,8 @@ class Detector:
             from .shard import longest_first as _lf
             perm = _lf([r.shape[0] for r in recordings])
             res = self.run_host([recordings[i] for i in perm], fs, params, mode=mode, stages=stages,
-                                want_y=want_y, log=log, options=options, longest_first=False)
+                                want_y=want_y, log=log, options=options, longest_first=False,
+                                resolve_ties=resolve_ties)
             out: List[dict] = [None] * len(recordings)
             for k, i in enumerate(perm):
                 out[i] = res[k]
@@ -266,12 +366,15 @@ class Detector:
             pcm = torch.from_numpy(host).to(self.device)
             res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log,
                            options=options)
+            if resolve_ties:
+                self.resolve_ties(res, params, stages)
             out = res.to_host()          # .cpu() waits for this stream only
             self.host_stream().synchronize()
         return out
 
     def run_env_host(self, envs: List[np.ndarray], sr: int, params: dict, stages: int,
-                     floors: Optional[List[np.ndarray]] = None, options: int = 0) -> List[dict]:
+                     floors: Optional[List[np.ndarray]] = None, options: int = 0,
+                     resolve_ties: bool = False) -> List[dict]:
         """Detection stages on host envelopes (drop-in for the env-level functions)."""
         torch = _torch()
         fo = np.zeros(len(envs) + 1, dtype=np.int64)
@@ -283,6 +386,8 @@ class Detector:
             if floors is not None:
                 out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
             self.run(None, fo, d.sr, params, stages=stages, out=out, d=d, options=options)
+            if resolve_ties:
+                self.resolve_ties(out, params, stages)
             res = out.to_host()
             self.host_stream().synchronize()
         return res

@@ -94,7 +94,8 @@ def _detect_local(items, idx, fs, params, mode, detector):
             d = design(f, params, log=False)
             if d.distance < 1:
                 raise ValueError(DISTANCE_MSG)
-            out = detector.run_host([data[i][1] for i in ids], f, params, mode=mode, stages=N.STAGE_ALL)
+            out = detector.run_host([data[i][1] for i in ids], f, params, mode=mode, stages=N.STAGE_ALL,
+                                    resolve_ties=True)
         except (ValueError, N.BpmxError) as exc:
             if isinstance(exc, N.BpmxError) and not exc.per_file:
                 raise                                   # HIP / device failure: the rank fails, not the files

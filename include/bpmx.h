@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BPMX_ABI_VERSION 1
+#define BPMX_ABI_VERSION 2
 
 /* sample formats of scipy.io.wavfile.read (bpm_analysis.py:1014) */
 enum bpmx_dtype { BPMX_DT_U8 = 0, BPMX_DT_I16 = 1, BPMX_DT_I32 = 2, BPMX_DT_F32 = 3, BPMX_DT_F64 = 4 };
@@ -79,7 +79,13 @@ enum bpmx_file_flag {
      * indices are those of every argsort order, so the reference's; with it
      * they may differ from the reference's on that machine. */
     BPMX_F_TROUGH_TIE = 32,  /* in the trough search find_peaks(-env) (:1070) */
-    BPMX_F_PEAK_TIE = 64     /* in the raw-peak search find_peaks(env, height=floor) (:227) */
+    BPMX_F_PEAK_TIE = 64,    /* in the raw-peak search find_peaks(env, height=floor) (:227) */
+    /* the distance filter of that search visited the candidates in the order
+     * the caller supplied (bpmx_run_ordered: np.argsort of the heights, as
+     * scipy's _select_by_peak_distance does); the matching TIE bit is then
+     * never set, since the order is the reference's and nothing is left open */
+    BPMX_F_TROUGH_ORDERED = 128,
+    BPMX_F_PEAK_ORDERED = 256
 };
 
 enum bpmx_option {
@@ -182,6 +188,39 @@ int64_t bpmx_decimated_length(int64_t n_frames, int32_t ds);
  * (a hipStream_t; NULL = default stream). */
 int bpmx_run(bpmx_ctx *ctx, const bpmx_params *params, const bpmx_batch *batch, const bpmx_out *out,
              void *stream);
+
+/* Resolving decisive ties in the reference's own order (BPMX_F_*_TIE).
+ *
+ * scipy's distance filter (_peak_finding_utils._select_by_peak_distance,
+ * called at scipy/signal/_peak_finding.py:976-980 from bpm_analysis.py:1070 and
+ * :227) visits the candidates in np.argsort(x[peaks]) order, highest last
+ * index first.  That order is numpy's, so only the host can produce it:
+ * a run with cand[s] set writes each recording's candidate list of search s
+ * (the local maxima, plateau midpoints, left by the height filter; ascending
+ * positions, per-file slices at D_f, n_cand[s][f] of them); the host computes
+ * rank = inverse of np.argsort(x[cand]) per recording; a run with rank[s] set
+ * (and use_rank[s][f] != 0) then decides the distance filter of recording f by
+ * rank alone — candidate k removes candidate j within `distance` iff
+ * rank[k] > rank[j] and k is kept — which is scipy's greedy loop exactly.
+ * Search 0 is the trough search find_peaks(-env) (:1070), 1 the raw-peak search
+ * find_peaks(env, height=floor) (:227).  The candidates of a search depend only
+ * on env (and the floor for search 1), so a rank computed from one run's list
+ * applies to any run on the same env (and floor).  All pointers are device
+ * pointers and optional (NULL: that part is not used); a run with an order
+ * object takes the one-workgroup find_peaks kernel for every recording.  Meant
+ * for the few recordings that carry a TIE bit (engine.Detector.resolve_ties).
+ */
+typedef struct {
+    int32_t *cand[2];           /* out: candidate positions, sum(Nd) entries, per-file slices at D_f */
+    int32_t *n_cand[2];         /* out: [n_files] candidate counts (with cand[s]) */
+    const int32_t *rank[2];     /* in: per candidate (same order as cand), its index in np.argsort(x[cand]) */
+    const int32_t *use_rank[2]; /* in: [n_files] nonzero = recording f's slice of rank[s] is set */
+} bpmx_peak_order;
+
+/* bpmx_run with a find_peaks visiting order / candidate export (above); order
+ * NULL = bpmx_run.  Never pipelined. */
+int bpmx_run_ordered(bpmx_ctx *ctx, const bpmx_params *params, const bpmx_batch *batch, const bpmx_out *out,
+                     const bpmx_peak_order *order, void *stream);
 
 /* Synthetic int16 recordings straight into HBM: file f gets seed seed0+f,
  * frames [frame_offsets[f], frame_offsets[f+1]) of pcm (device). */

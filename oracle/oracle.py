@@ -277,6 +277,43 @@ def rolling_quantile(v: np.ndarray, w: int, minp: int, q: float) -> np.ndarray:
     return out
 
 
+def noise_floor_from_raw(env: np.ndarray, raw: np.ndarray, d: Derived, params: dict):
+    """_calculate_dynamic_noise_floor after its trough search (bpm_analysis.py:1073-1117)
+    from a given raw trough list -> (floor, troughs, flags): the static fallback
+    (< 5 troughs), the draft floor (interp + centred rolling quantile +
+    bfill/ffill), the sanitize loop, the final floor or the draft fallback, the
+    all-NaN fallback.  Composes this module's C restatements; used with
+    find_peaks_numpy_order's troughs (noise_floor_numpy_order)."""
+    env = np.ascontiguousarray(env, dtype=np.float64)
+    raw = np.asarray(raw, dtype=np.int64)
+    q = params["noise_floor_quantile"]
+    if raw.size < 5:                                                          # :1073-1077
+        return np.full(env.size, quantile(env, q)), raw, 1
+    draft = rolling_quantile(interp_dense(raw, env), d.noise_window, 3, q)   # :1081-1086
+    mult = params.get("trough_rejection_multiplier", 4.0)
+    kept = np.array([t for t in raw if not np.isnan(draft[t]) and env[t] <= mult * draft[t]], dtype=np.int64)
+    flags = 0
+    if kept.size > 2:                                                         # :1101-1106
+        floor = rolling_quantile(interp_dense(kept, env), d.noise_window, 3, q)
+    else:                                                                     # :1107-1110
+        floor, flags = draft, 2
+    if np.isnan(floor).all():                                                 # :1113-1115
+        floor, flags = np.full(env.size, quantile(env, 0.1)), flags | 4
+    return floor, kept, flags
+
+
+def noise_floor_numpy_order(env: np.ndarray, d: Derived, params: dict):
+    """_calculate_dynamic_noise_floor with its trough search in numpy's argsort
+    order (find_peaks_numpy_order), i.e. the reference's answer on this
+    machine when a decisive tie decides the troughs -> (floor, troughs, flags,
+    raw troughs).  Small cases only."""
+    env = np.ascontiguousarray(env, dtype=np.float64)
+    raw = find_peaks_numpy_order(env, distance=d.distance, negate=True,
+                                 prominence=quantile(env, params["trough_prominence_quantile"]))
+    floor, kept, flags = noise_floor_from_raw(env, raw, d, params)
+    return floor, kept, flags, raw
+
+
 def noise_floor(env: np.ndarray, d: Derived, params: dict):
     """_calculate_dynamic_noise_floor -> (floor f64, troughs i64, flags)."""
     env = np.ascontiguousarray(env, dtype=np.float64)

@@ -114,7 +114,7 @@ class _OracleDetector:
     gather (the GPU detector is covered by the -m gpu tests)."""
     device = torch.device("cpu")
 
-    def run_host(self, recs, fs, params, mode="native", stages=7):
+    def run_host(self, recs, fs, params, mode="native", stages=7, resolve_ties=False):
         from oracle import oracle as O
         ds = O.derive(fs, params).ds
         out = []

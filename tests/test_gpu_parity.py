@@ -125,13 +125,92 @@ def test_tie_goldens_flagged(det, name):
     assert bool(p["flags"] & N.F_PEAK_TIE) == otie
     if not otie:
         assert _same(p["peaks"], g["peaks"])
-    # the same envelopes through the long-recording kernels (k_fpl_*) and the
-    # one-workgroup global-memory kernel: same outputs and flags
+    # the same envelopes through the one-workgroup global-memory kernel
+    # (k_find_peaks): same outputs and flags
     for opt in (N.OPT_PEAKS_GLOBAL,):
         r2 = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR, options=opt)[0]
         assert _same(r2["troughs"], ot) and r2["flags"] == ofl
         p2 = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_PEAKS, floors=[g["floor"]], options=opt)[0]
         assert _same(p2["peaks"], opk) and p2["flags"] == p["flags"]
+    # FLOOR | PEAKS in one run: the peak launch of k_find_peaks_lds takes the
+    # trough launch's extrema lists (bpmx_fpscan.h) on these plateau- and
+    # tie-heavy envelopes; peaks and PEAK_TIE as the oracle's on its own floor
+    opk2, otie2 = O.raw_peaks(g["env"], of, d, g["params"], return_tie=True)
+    for opt in (0, N.OPT_PEAKS_GLOBAL):
+        c = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS, options=opt)[0]
+        assert _same(c["floor"], of) and _same(c["troughs"], ot) and _same(c["peaks"], opk2)
+        assert c["flags"] == ofl | (N.F_PEAK_TIE if otie2 else 0)
+
+
+def _numpy_order_answer(env, d, params, floor=None):
+    """The reference's answer on this machine (oracle restatement with numpy's
+    own argsort order in find_peaks' distance filter)."""
+    nf, nt, nfl, nraw = O.noise_floor_numpy_order(env, d, params)
+    h = nf if floor is None else floor
+    pk = O.find_peaks_numpy_order(env, height=h, distance=d.distance,
+                                  prominence=O.quantile(env, params["peak_prominence_quantile"]))
+    return nf, nt, nfl, nraw, pk
+
+
+@pytest.mark.parametrize("name", G.names(kind="env", prefix="env_ties"))
+def test_tie_goldens_resolved(det, name):
+    """Decisive ties re-decided in numpy's argsort order (engine.resolve_ties,
+    bpmx_run_ordered): the reference-made tie goldens' troughs, floor and raw
+    peaks come out exactly, through the engine and through the drop-in."""
+    from bpm_analysis_amd import _native as N, dropin
+    g = G.load(name)
+    sr = int(g["sr"])
+    d = G.env_derived(g)
+    nf, nt, nfl, nraw, npk = _numpy_order_answer(g["env"], d, g["params"])
+    r = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR, resolve_ties=True)[0]
+    assert _same(r["troughs"], nt) and _same(r["floor"], nf)
+    assert r["n_raw_troughs"] == len(nraw)
+    assert r["flags"] & TIE_BITS == 0 and r["flags"] & N.F_TROUGH_ORDERED
+    p = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_PEAKS, floors=[g["floor"]], resolve_ties=True)[0]
+    c = det.run_env_host([g["env"]], sr, g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS, resolve_ties=True)[0]
+    assert _same(c["troughs"], nt) and _same(c["floor"], nf) and _same(c["peaks"], npk)
+    assert p["flags"] & TIE_BITS == 0 and c["flags"] & TIE_BITS == 0
+    # the reference's own outputs (made in the build container, whose numpy
+    # argsort orders these heights as this box's does: the oracle's numpy-order
+    # raw troughs equal the reference's here too)
+    assert _same(nraw, g["raw_troughs"])
+    assert _same(r["troughs"], g["troughs"]) and _same(r["floor"], g["floor"])
+    assert _same(p["peaks"], g["peaks"]) and _same(c["peaks"], g["peaks"])
+    # the drop-in (bpm_analysis.py:1064-1117, :223-229 signatures)
+    fs, tr = dropin._calculate_dynamic_noise_floor(g["env"], sr, g["params"])
+    assert _same(tr, nt) and _same(fs.values, nf)
+    assert _same(dropin.find_raw_peaks(g["env"], sr, g["params"], g["floor"]), p["peaks"])
+
+
+def test_tie_resolution_in_a_batch(det):
+    """Many quantised (tie-heavy) envelopes with untied neighbours in one batch:
+    the flagged recordings re-run as a sub-batch and are written back in place;
+    every recording equals the numpy-order oracle, untied ones are untouched."""
+    from bpm_analysis_amd import _native as N
+    rng = np.random.default_rng(5)
+    params = dict(G.BASE_PARAMS)
+    sr = 302
+    d = G.env_derived({"params": params, "sr": sr})
+    envs = []
+    for k in range(24):
+        n = int(rng.integers(2500, 7000))
+        t = np.arange(n)
+        base = 5 + 100 * np.sin(t / 40.0) ** 2
+        e = np.round(base + rng.random(n) * 6) / 3.0 if k % 3 else base + rng.random(n)
+        envs.append(np.ascontiguousarray(e, dtype=np.float64))
+    plain = det.run_env_host(envs, sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS)
+    res = det.run_env_host(envs, sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS, resolve_ties=True)
+    n_flagged = 0
+    for e, a, r in zip(envs, plain, res):
+        nf, nt, nfl, nraw, npk = _numpy_order_answer(e, d, params)
+        assert _same(r["troughs"], nt) and _same(r["floor"], nf) and _same(r["peaks"], npk)
+        assert r["n_raw_troughs"] == len(nraw)
+        assert r["flags"] & TIE_BITS == 0
+        if a["flags"] & TIE_BITS:
+            n_flagged += 1
+        else:
+            assert _same(a["troughs"], r["troughs"]) and _same(a["peaks"], r["peaks"]) and a["flags"] == r["flags"]
+    assert n_flagged >= 8
 
 
 def test_vulpine_reference_pipeline_and_known_answer(det):
@@ -146,6 +225,15 @@ def test_vulpine_reference_pipeline_and_known_answer(det):
     assert _same(fl["peaks"], g["log_peaks"])
     assert fl["flags"] & TIE_BITS == N.F_TROUGH_TIE
     assert len(np.intersect1d(fl["troughs"], g["log_troughs"])) >= 1345
+    # resolved in numpy's order: the reference's troughs and floor on this
+    # machine (oracle numpy-order restatement), raw peaks still the log's
+    d = O.derive(int(g["fs"]), g["params"])
+    assert d.sr == 302
+    nf, nt, nfl, nraw, npk = _numpy_order_answer(env, d, g["params"])
+    rs = det.run_env_host([env], 302, g["params"], N.STAGE_FLOOR | N.STAGE_PEAKS, resolve_ties=True)[0]
+    assert _same(rs["troughs"], nt) and _same(rs["floor"], nf) and _same(rs["peaks"], npk)
+    assert rs["flags"] & TIE_BITS == 0 and rs["flags"] & N.F_TROUGH_ORDERED
+    assert _same(rs["peaks"], g["log_peaks"])
 
 
 def test_synthetic_batch_vs_oracle(det):

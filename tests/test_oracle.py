@@ -67,6 +67,30 @@ def test_oracle_tie_goldens(name):
     assert flags & O.F_TROUGH_TIE
     pk, ptie = O.raw_peaks(env, g["floor"], d, p, return_tie=True)
     assert ptie or np.array_equal(pk, g["peaks"])
+    # (3) the whole noise floor in numpy's order (the GPU tie resolution's
+    # checker): the reference's troughs and floor, bit for bit
+    nf, nt, nfl, nraw = O.noise_floor_numpy_order(env, d, p)
+    assert np.array_equal(nraw, g["raw_troughs"])
+    assert np.array_equal(nt, g["troughs"])
+    assert np.array_equal(nf, g["floor"], equal_nan=True)
+    assert (nfl & 3) == (int(g["flags"]) & 3)
+
+
+def test_noise_floor_from_raw_matches_c_restatement():
+    """noise_floor_from_raw (the Python composition behind the numpy-order
+    floor) equals bpmx_oracle.c's noise floor when both start from the same raw
+    troughs (the stable order's, on every golden envelope without a tie)."""
+    for name in [n for n in G.names(kind="env") if not n.startswith("env_ties")]:
+        g = G.load(name)
+        d = G.env_derived(g)
+        env, p = g["env"], g["params"]
+        raw = O.find_peaks(env, distance=d.distance, negate=True,
+                           prominence=O.quantile(env, p["trough_prominence_quantile"]))
+        f1, t1, fl1 = O.noise_floor(env, d, p)
+        f2, t2, fl2 = O.noise_floor_from_raw(env, raw, d, p)
+        assert np.array_equal(f1, f2, equal_nan=True), name
+        assert np.array_equal(t1, t2), name
+        assert (fl1 & 7) == fl2, name
 
 
 def test_tie_report_is_exact():
