@@ -322,6 +322,27 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     }
     const int64_t sumnd = doff[F], sumb = boff[F];
     if (sumnd == 0) return fail(BPMX_E_ARG, "empty recordings");
+    /* int16 PCM whose base is not 16-byte aligned but sits a whole number of
+     * frames past a 16-byte boundary (e.g. a pipelined chunk or any sub-range
+     * of an aligned buffer): the kernels read from that boundary and every
+     * recording's frame offset moves up by the difference, so the matrix-core
+     * block kernel (16-byte aligned base) serves it.  Its projections are exact
+     * integer sums and its tiles start at each recording's own first block, so
+     * a recording's envelope does not depend on where it lies in the buffer
+     * (include/bpmx.h, bpmx_set_pipeline).  The boundary is in the same page as
+     * the base, and the kernels drop what lies before a recording's start. */
+    bpmx_batch b_shift;
+    if (do_env && P->dtype == BPMX_DT_I16 && B->pcm) {
+        const uintptr_t mis = (uintptr_t)B->pcm & 15;
+        const uintptr_t fb = (uintptr_t)2 * (uintptr_t)P->channels;
+        if (mis != 0 && mis % fb == 0) {
+            const int64_t sh = (int64_t)(mis / fb);
+            for (int f = 0; f <= F; ++f) foff[f] += sh;
+            b_shift = *B;
+            b_shift.pcm = (const void *)((const char *)B->pcm - mis);
+            B = &b_shift;
+        }
+    }
 
     int rc = BPMX_OK;
     std::vector<int64_t> geo;

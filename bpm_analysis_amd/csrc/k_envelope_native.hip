@@ -2026,13 +2026,10 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         HilbPlan hp;
         size_t hlds = 0;
         HbTables *ht = nullptr;
-        if (nd > 15 && (doff[f0] & 1) == 0 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) &&
+        if (nd > 15 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) &&
             (ht = hb_tables(ctx, nd, P->env_window, &hp, &hlds, s, &rc)) != nullptr) {
             if (rc != BPMX_OK) return rc;
-            /* recordings of the run all start at even offsets? (double2 loads) */
-            bool even = true;
-            for (int f = f0; f < f1; ++f) even = even && (doff[f] & 1) == 0;
-            if (even) {
+            {                                                    /* any decimated offset (k_hilbert_env's loads) */
                 HilbArgs a;
                 a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
                 a.tabs = ht->dev; a.env = O->env; a.stamps = nullptr;

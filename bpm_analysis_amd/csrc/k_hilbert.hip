@@ -444,19 +444,27 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     S.twl = S.twh + P.ntwh;
     S.pt = S.twl + 128;
     const int64_t d0 = A.doff[f];
-    const double2 *y2 = (const double2 *)(A.yd + d0);              /* doff is even: 16-B aligned (host checks) */
+    /* yd as complex pairs: 16-byte loads when the recording starts at an even
+     * decimated offset, two 8-byte loads otherwise (same values, so a
+     * recording's envelope does not depend on its place in the batch) */
+    const bool odd = (d0 & 1) != 0;
+    const double2 *y2a = (const double2 *)(A.yd + (d0 & ~(int64_t)1));
+    const double *y1 = A.yd + d0;
+    auto y2 = [&](int m) -> double2 {
+        return odd ? make_double2(y1[2 * m], y1[2 * m + 1]) : y2a[m];
+    };
     /* a leading radix-2 stage over the whole transform (B = M) is fused into
      * the load, a trailing one of the inverse into the magnitude */
     const bool r2 = P.rad[0] == 2 && P.B[0] == M;
     const int H = M / 2;
     for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab + P.nrtab; i += HB_T) S.twh[i] = A.tabs[i];
     if (!r2)
-        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2[m];
+        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2(m);
     __syncthreads();
     STAMP_DECL
     if (r2) {
         for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIF radix 2: L = M / 2, twiddle W_N^(2t) */
-            const double2 a = y2[t], b = y2[t + H], d = csub(a, b);
+            const double2 a = y2(t), b = y2(t + H), d = csub(a, b);
             S.x[t] = cadd(a, b);
             S.x[t + H] = t ? cmul(d, S.tw(2 * t)) : d;
         }
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     };
     if (r2) {
         for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIT radix 2 (conjugate twiddle before), then |.| */
-            const double2 ya = y2[t], yb = y2[t + H];
+            const double2 ya = y2(t), yb = y2(t + H);
             const double2 a = S.x[t];
             double2 b = S.x[t + H];
             if (t) b = cmulc(b, S.tw(2 * t));
@@ -515,7 +523,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
             S.x[t + H] = mag2(csub(a, b), yb);
         }
     } else {
-        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = mag2(S.x[m], y2[m]);
+        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = mag2(S.x[m], y2(m));
     }
     __syncthreads();
     STAMP(6);

@@ -66,7 +66,8 @@ enum bpmx_file_flag {
     BPMX_F_STATIC_FLOOR = 1, /* < 5 troughs: constant quantile floor, troughs unsanitised (:1073-1077) */
     BPMX_F_DRAFT_FLOOR = 2,  /* <= 2 sanitised troughs: draft floor kept (:1107-1110) */
     BPMX_F_NAN_FLOOR = 4,    /* all-NaN floor replaced by quantile(env, 0.1) (:1113-1115) */
-    BPMX_F_TOO_SHORT = 8,    /* Nd <= 15: scipy filtfilt raises ValueError; no outputs */
+    BPMX_F_TOO_SHORT = 8,    /* Nd <= 15: scipy filtfilt raises ValueError; no outputs (its slices of the
+                                output arrays are left as they were; counts are 0) */
     BPMX_F_BAD_WINDOW = 16,  /* noise_window < min_periods and >= 5 troughs: pandas rolling() raises
                                 ValueError (:1085); floor/peaks of this recording are not meaningful */
     /* find_peaks' distance filter visits candidates in np.argsort(height) order
@@ -246,9 +247,10 @@ int bpmx_profile_only(bpmx_ctx *ctx, const char *label);
  * stream restricted to det_cus other CUs when det_cus > 0, else on the
  * caller's stream), so the HBM-bound envelope kernels overlap the
  * latency-bound detection kernels.  Same outputs as an unpipelined run: every
- * index, count and flag identical; env, y and floor bit-identical in reference
- * mode and within the native tolerance in native mode (a chunk's PCM base may
- * lose the 16-byte alignment the int16 matrix-core block kernel needs).
+ * index, count and flag identical, env, y and floor bit-identical, in both
+ * modes (a recording's outputs do not depend on where its PCM lies: an int16
+ * base a whole number of frames past a 16-byte boundary is read from that
+ * boundary, so a chunk keeps the matrix-core block kernel).
  * Pipeline sub-contexts share the root context's side streams, which carry no
  * CU mask.  chunks = 0 (the default) turns it off.  Waits for the device. */
 int bpmx_set_pipeline(bpmx_ctx *ctx, int chunks, int env_cus, int det_cus);
