@@ -382,9 +382,12 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* find_peaks' candidate lists and the run's scan record (bpmx_fpscan.h:
      * the trough launch's scan, reused by the peak launch) */
     int32_t *cand = nullptr, *vcand = nullptr, *fp_scan = nullptr;
+    double *cval = nullptr, *vval = nullptr;
     if (do_floor || do_peaks) {
         cand = (int32_t *)ctx->buf("cand", (size_t)sumnd * 4, &rc);
         vcand = (int32_t *)ctx->buf("vcand", (size_t)sumnd * 4, &rc);
+        cval = (double *)ctx->buf("cval", (size_t)sumnd * 8, &rc);
+        vval = (double *)ctx->buf("vval", (size_t)sumnd * 8, &rc);
         fp_scan = (int32_t *)ctx->buf("fp_scan", (size_t)F * 4 * (1 + 2 * FPS_NW), &rc);
         if (rc != BPMX_OK) return rc;
     }
@@ -609,7 +612,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     const dim3 g_dch((unsigned)((maxnd / 2 + 1 + FPC_S - 1) / FPC_S), (unsigned)F);
 #define FIND_PEAKS(A, TAG)                                                                                  \
     do {                                                                                                   \
-        (A).vcand = vcand; (A).fallback = fp_fb; (A).only = nullptr; (A).flags = (int32_t *)O->flags;     \
+        (A).vcand = vcand; (A).cval = cval; (A).vval = vval; (A).fallback = fp_fb; (A).only = nullptr; (A).flags = (int32_t *)O->flags;     \
         (A).lds_nmax = fp_long ? FPL_NMIN : INT64_MAX;                                                     \
         if (!fp_global) {                                                                                  \
             LAUNCH(ctx, s, "k_find_peaks[" TAG "]", k_find_peaks_lds, dim3(F), dim3(1024), 0, s, (A));    \

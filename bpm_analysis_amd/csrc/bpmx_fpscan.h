@@ -5,7 +5,11 @@
  * 1024-thread workgroup scans its own contiguous run [w0, w1) 64 positions at
  * a time and compacts, in order, the local maxima (plateau midpoints) into
  * mp[w0 - 1 ..] and the valleys (strict local minima / flat bottoms, also at
- * their plateau midpoints; only their values are used) into vp[w0 - 1 ..].
+ * their plateau midpoints; only their values are used) into vp[w0 - 1 ..],
+ * with their values x (equal along a plateau) in mv / vv at the same indices:
+ * the consumers read the extrema's values from these lists instead of
+ * gathering them from the envelope (a recording's envelope does not stay in
+ * L2 between the scan and the gathers: ~2000 scattered cache lines each).
  *
  * The maxima of -env are the valleys of env and its valleys env's maxima, at
  * the same positions in the same per-wave runs, so one scan serves both
@@ -35,8 +39,8 @@ __device__ __forceinline__ void fp_scan_run(int64_t n, int wid, int64_t &w0, int
 
 /* one wave: x(i) = the signed value at position i (0 <= i < n) */
 template <class X>
-__device__ __forceinline__ void fp_scan_wave(X x, int64_t n, int64_t w0, int64_t w1, int32_t *mp, int32_t *vp, int &cm,
-                                             int &cv) {
+__device__ __forceinline__ void fp_scan_wave(X x, int64_t n, int64_t w0, int64_t w1, int32_t *mp, int32_t *vp,
+                                             double *mv, double *vv, int &cm, int &cv) {
     const int lane = lane_id();
     const unsigned long long lt = (1ull << lane) - 1ull;
     cm = cv = 0;
@@ -67,8 +71,16 @@ __device__ __forceinline__ void fp_scan_wave(X x, int64_t n, int64_t w0, int64_t
             }
         }
         const unsigned long long bm = __ballot(ism), bv = __ballot(isv);
-        if (ism) mp[w0 - 1 + cm + __popcll(bm & lt)] = pk;
-        if (isv) vp[w0 - 1 + cv + __popcll(bv & lt)] = pk;
+        if (ism) {
+            const int64_t k = w0 - 1 + cm + __popcll(bm & lt);
+            mp[k] = pk;
+            mv[k] = xc;
+        }
+        if (isv) {
+            const int64_t k = w0 - 1 + cv + __popcll(bv & lt);
+            vp[k] = pk;
+            vv[k] = xc;
+        }
         cm += __popcll(bm);
         cv += __popcll(bv);
         xedge = __shfl(xc, 63);

@@ -116,6 +116,7 @@ struct PeakArgs {
     int32_t *run_out;      /* optional [F]: 1 if nout >= run_min */
     int32_t run_min;
     int32_t *vcand;        /* k_find_peaks_lds: scratch [sumNd], valley positions */
+    double *cval, *vval;   /* k_find_peaks_lds: scratch [sumNd], the values of cand / vcand's extrema */
     int32_t *fallback;     /* k_find_peaks_lds: [F] out, 1 = too many maxima for LDS (k_find_peaks takes it) */
     const int32_t *only;   /* k_find_peaks / k_fpl_*: [F] or null, process only recordings with only[f] != 0 */
     int64_t lds_nmax;      /* k_find_peaks_lds: hand recordings longer than this over (fallback = 1) */

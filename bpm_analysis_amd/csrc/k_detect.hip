@@ -665,18 +665,24 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     int64_t w0, w1;
     fp_scan_run(n, wid, w0, w1);
     int32_t *mp_g, *vp_g;
+    double *mv_g, *vv_g, vsg = 1.0;                          /* the extrema's values, made for the lists' sign */
     int cm, cv;                                              /* wave-uniform counts */
     if (so != 0) {
         const bool direct = so == sgn;
         mp_g = (direct ? A.cand : A.vcand) + d0;
         vp_g = (direct ? A.vcand : A.cand) + d0;
+        mv_g = (direct ? A.cval : A.vval) + d0;
+        vv_g = (direct ? A.vval : A.cval) + d0;
+        vsg = direct ? 1.0 : -1.0;
         const int c0 = A.scan_cnt[((int64_t)f * NW + wid) * 2], c1 = A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1];
         cm = direct ? c0 : c1;
         cv = direct ? c1 : c0;
     } else {
         mp_g = A.cand + d0;
         vp_g = A.vcand + d0;
-        fp_scan_wave([&](int64_t i) { return sg * e[i]; }, n, w0, w1, mp_g, vp_g, cm, cv);
+        mv_g = A.cval + d0;
+        vv_g = A.vval + d0;
+        fp_scan_wave([&](int64_t i) { return sg * e[i]; }, n, w0, w1, mp_g, vp_g, mv_g, vv_g, cm, cv);
         if (A.scan_ok && lane == 0) {
             A.scan_cnt[((int64_t)f * NW + wid) * 2] = cm;
             A.scan_cnt[((int64_t)f * NW + wid) * 2 + 1] = cv;
@@ -704,7 +710,7 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
     const int64_t dist = A.distance;
     for (int t = lane; t < cm; t += 64) {                    /* this wave's run of maxima */
         const int32_t p = mp_g[w0 - 1 + t];
-        const double xv = sg * e[p];
+        const double xv = vsg * mv_g[w0 - 1 + t];
         const int k = om + t;
         s_mp[k] = p;
         s_mh[k] = xv;
@@ -720,9 +726,8 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
      * wave's first extremum is a maximum */
     const int vfirst = (cm > 0 && (cv == 0 || mp_g[w0 - 1] < vp_g[w0 - 1])) ? 1 : 0;
     for (int t = lane; t < cv; t += 64) {
-        const int32_t pv = vp_g[w0 - 1 + t];
         const int lo = om + t + vfirst;
-        const double val = sg * e[pv];
+        const double val = vsg * vv_g[w0 - 1 + t];
         if (lo == 0 || lo == M) s_vv[lo] = fmin(s_vv[lo], val);   /* edge gaps: at most one valley each */
         else s_vv[lo] = val;
     }
