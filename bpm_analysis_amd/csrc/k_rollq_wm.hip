@@ -672,6 +672,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     unsigned long long dq[8] = {0};   /* tools/rqbench -DRQ_DIAG_Q, wave 0: blocks, need, partial members, collect trips, cursor trips, collected */
 #endif
     int vfirst = INT_MAX, vlast = -1;
+#ifdef RQ_DIAG_W
+    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();   /* tools/rqbench -DRQ_DIAG_W: per-wave output phase */
+#endif
     {
         const int NBLK = (int)((o1 - o0 + 63) >> 6);
         const int NBW = (NBLK + NWV - 1) / NWV;
@@ -877,6 +880,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             STAMP(6);
         }
     }
+#ifdef RQ_DIAG_W
+    if (lane == 0 && A.stamps) A.stamps[blockIdx.x * 16 + wid] = __builtin_amdgcn_s_memtime() - tw0;
+#endif
     for (int o = 32; o > 0; o >>= 1) {
         vfirst = min(vfirst, __shfl_xor(vfirst, o));
         vlast = max(vlast, __shfl_xor(vlast, o));
@@ -888,7 +894,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     __threadfence_block();
     __syncthreads();
     STAMP(7);                                                /* (the other waves' query tail) */
+#ifndef RQ_DIAG_W
     STAMP_FLUSH(A.stamps);
+#endif
 #ifdef RQ_DIAG_Q
     if (threadIdx.x == 0 && A.stamps)
         for (int k = 0; k < 8; ++k) A.stamps[blockIdx.x * 16 + 8 + k] = dq[k];

@@ -101,6 +101,19 @@ int main(int argc, char **argv) {
                ms[F * 9 / 10], ms[F * 99 / 100], ms[F - 1]);
     }
 #endif
+#ifdef RQ_DIAG_W
+    {
+        double a[16] = {0}, mx[16] = {0};
+        for (int f = 0; f < F; ++f)
+            for (int k = 0; k < 16; ++k) {
+                a[k] += (double)st[(size_t)f * 16 + k];
+                mx[k] = std::max(mx[k], (double)st[(size_t)f * 16 + k]);
+            }
+        printf("output phase cycles per wave (mean / max over workgroups):");
+        for (int k = 0; k < 16; ++k) printf(" w%d %.0f/%.0f", k, a[k] / F, mx[k]);
+        printf("\n");
+    }
+#endif
 #ifdef RQ_DIAG_Q
     {
         double a[8] = {0};
