@@ -676,6 +676,11 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* ---- FLOOR ---- */
     if (do_floor) {
         int64_t *rawt = (int64_t *)ctx->buf("raw_troughs", (size_t)sumnd * 8, &rc);
+        /* env at the raw and at the sanitised troughs, beside the indices (the
+         * trough search and k_sanitize write them; the floor kernels read them
+         * instead of gathering a cache line of env per trough) */
+        double *rawv = (double *)ctx->buf("raw_trough_vals", (size_t)sumnd * 8, &rc);
+        double *trv = (double *)ctx->buf("trough_vals", (size_t)sumnd * 8, &rc);
         double *dense = (double *)ctx->buf("dense", (size_t)sumnd * 8, &rc);
         double *draft = (double *)ctx->buf("draft", (size_t)sumnd * 8, &rc);
         if (rc != BPMX_OK) return rc;
@@ -683,7 +688,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             PeakArgs a;
             a.env = O->env; a.height = nullptr; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
             a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_TROUGH; a.n_files = F; a.distance = P->distance;
-            a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.nout = d_nraw;
+            a.sign = -1.0; a.cand = cand; a.state = state; a.out = rawt; a.outv = rawv; a.nout = d_nraw;
             a.run_out = d_run1; a.run_min = 5; a.tie_bit = BPMX_F_TROUGH_TIE;
             a.scan_ok = fp_scan; a.scan_cnt = fp_scan + F;
             set_order(a, 0);
@@ -748,9 +753,9 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             return BPMX_OK;
         };
         auto rollq = [&](const int32_t *run, const int64_t *tr, const int32_t *ntr, double *outp,
-                         int32_t *allnan) -> int {
+                         int32_t *allnan, const double *tv) -> int {
             RollqArgs a;
-            a.dense = dense; a.doff = d_doff; a.troughs = tr; a.run = run; a.n_files = F;
+            a.dense = dense; a.doff = d_doff; a.troughs = tr; a.tv = tv; a.run = run; a.n_files = F;
             a.env = O->env; a.ntr = ntr;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.cap = cap; a.q = P->noise_floor_q;
             a.out = outp; a.allnan = allnan; a.wm_max = use_wm ? WM_MMAX : 0;
@@ -837,7 +842,8 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             d_exact = draft_masks;                             /* zeroed by k_init_out */
             d_runfb = draft_masks + F;
             DraftBoundArgs a;
-            a.env = O->env; a.doff = d_doff; a.raw = rawt; a.nraw = d_nraw; a.run = d_run1; a.n_files = F;
+            a.env = O->env; a.doff = d_doff; a.raw = rawt; a.rawv = rawv; a.nraw = d_nraw; a.run = d_run1;
+            a.n_files = F;
             a.window = (int32_t)W; a.min_periods = P->min_periods; a.q = P->noise_floor_q; a.mult = P->reject_mult;
             a.dec = tdec; a.exact = d_exact;
             a.local_m = (P->options & BPMX_OPT_DRAFT_GLOBAL_RANK) ? INT_MAX : DB_LOCAL_M;
@@ -858,16 +864,17 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
             LAUNCH(ctx, s, "k_draft_points[wide]", k_draft_points<4>, dim3(F, gp), dim3(DB_T), 0, s, a);
         }
-        if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
+        if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
         {
             SanitizeArgs a;
             a.env = O->env; a.draft = draft; a.doff = d_doff; a.active = d_active; a.raw = rawt; a.nraw = d_nraw;
+            a.rawv = rawv; a.outv = trv;
             a.n_files = F; a.mult = P->reject_mult; a.out = O->troughs; a.nout = O->n_troughs; a.flags = O->flags;
             a.run2 = d_run2; a.dec = tdec; a.exact = d_exact; a.run_fb = d_runfb;
             LAUNCH(ctx, s, "k_sanitize", k_sanitize, dim3(F), dim3(256), 0, s, a);
         }
-        if (bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1)) != BPMX_OK) return rc;
-        if ((rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2)) != BPMX_OK) return rc;
+        if (bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
+        if ((rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2, trv)) != BPMX_OK) return rc;
         {
             FinalArgs a;
             a.draft = draft; a.doff = d_doff; a.active = d_active; a.qv = qv; a.allnan_draft = d_an1;

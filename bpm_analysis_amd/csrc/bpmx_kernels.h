@@ -112,6 +112,7 @@ struct PeakArgs {
     int32_t *cand;         /* scratch [sumNd] */
     uint8_t *state;        /* scratch [sumNd] */
     int64_t *out;          /* [sumNd] */
+    double *outv = nullptr;  /* optional [sumNd]: env at each output index (sign removed), beside out */
     int32_t *nout;         /* [F] */
     int32_t *run_out;      /* optional [F]: 1 if nout >= run_min */
     int32_t run_min;
@@ -213,6 +214,7 @@ struct RollqArgs {
     int32_t *allnan;         /* [F] */
     int32_t wm_max;          /* k_rolling_quantile skips files with n <= wm_max (k_rollq_wm took them) */
     const double *env;       /* k_rollq_wm: interpolate dense from env at the troughs itself ... */
+    const double *tv;        /* ... taken from tv (env at each trough, beside troughs) when set */
     const int32_t *ntr;      /* ... when the file has <= WM_TRMAX of them (else read dense) */
     int64_t chunk;           /* k_rolling_quantile: outputs per workgroup (blockIdx.y = chunk of the file) */
     int32_t *vfirst, *vlast; /* [F] first / last valid output over all chunks (k_rollq_fill reads them) */
@@ -236,9 +238,11 @@ struct SanitizeArgs {
     const int64_t *doff;
     const int32_t *active;
     const int64_t *raw;      /* raw troughs (slices at doff) */
+    const double *rawv;      /* env at the raw troughs (find_peaks' outv), beside raw */
     const int32_t *nraw;
     int32_t n_files;
     double mult;
+    double *outv;            /* env at the kept troughs, beside out */
     int64_t *out;
     int32_t *nout;
     int32_t *flags;
@@ -257,6 +261,7 @@ struct DraftBoundArgs {
     const double *env;
     const int64_t *doff;
     const int64_t *raw;      /* raw troughs */
+    const double *rawv;      /* env at the raw troughs (find_peaks' outv), beside raw: no gathers from env */
     const int32_t *nraw;
     const int32_t *run;      /* [F] files with >= 5 raw troughs */
     int32_t n_files, window, min_periods;

@@ -582,7 +582,10 @@ __global__ __launch_bounds__(FP_T, BPMX_FP_LB) void k_find_peaks(PeakArgs A) {
         const bool keep = j < m && ld_state(&st[j]) == ST_FINAL;
         int tot;
         const int off = block_scan_flag<FP_T>(keep, sh, &tot);
-        if (keep) out[w + off] = cp[j];
+        if (keep) {
+            out[w + off] = cp[j];
+            if (A.outv) A.outv[d0 + w + off] = sg * cval(j);
+        }
         w += tot;
     }
     if (tid == 0) {
@@ -951,7 +954,10 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         const bool keep = j < M && s_st[j] == ST_FINAL;
         int tot;
         const int off = block_scan_flag<FP_T>(keep, sh, &tot);
-        if (keep) out[w + off] = s_mp[j];
+        if (keep) {
+            out[w + off] = s_mp[j];
+            if (A.outv) A.outv[d0 + w + off] = sg * s_mh[j];
+        }
         w += tot;
     }
     if (tid == 0) {

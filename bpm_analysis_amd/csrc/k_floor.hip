@@ -620,30 +620,34 @@ __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
     int64_t *out = A.out + d0;
     const int m = A.nraw[f];
     const int tid = threadIdx.x;
+    const double *rawv = A.rawv + d0;
+    double *outv = A.outv + d0;
     if (m < 5) {
-        for (int j = tid; j < m; j += 256) out[j] = raw[j];
+        for (int j = tid; j < m; j += 256) { out[j] = raw[j]; outv[j] = rawv[j]; }
         if (tid == 0) { A.nout[f] = m; A.flags[f] |= BPMX_F_STATIC_FLOOR; A.run2[f] = 0; }
         return;
     }
-    const double *env = A.env + d0, *draft = A.draft + d0;
+    const double *draft = A.draft + d0;
     const bool exact = !A.dec || A.exact[f];
     int w = 0;
     for (int c0 = 0; c0 < m; c0 += 256) {
         const int j = c0 + tid;
         bool keep = false;
         int64_t t = 0;
+        double tv = 0.0;
         if (j < m) {
             t = raw[j];
+            tv = rawv[j];                                    /* env[t] */
             if (exact) {
                 const double fl = draft[t];
-                keep = (fl == fl) && env[t] <= A.mult * fl;
+                keep = (fl == fl) && tv <= A.mult * fl;
             } else {
                 keep = A.dec[d0 + j] == 1;
             }
         }
         int tot;
         const int off = block_scan_flag<256>(keep, sh, &tot);
-        if (keep) out[w + off] = t;
+        if (keep) { out[w + off] = t; outv[w + off] = tv; }
         w += tot;
     }
     if (tid == 0) {
@@ -982,7 +986,7 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         return;
     }
     const int64_t *raw = A.raw + d0;
-    const double *env = A.env + d0;
+    const double *rawv = A.rawv + d0;                        /* env at the raw troughs */
     const int64_t W = A.window, t0 = raw[0], off = (W - 1) / 2;
     if (tid == 0) { s_vf = INT_MAX; s_vl = -1; }
     __syncthreads();
@@ -1036,9 +1040,8 @@ __global__ __launch_bounds__(DB_T) void k_draft_bounds(DraftBoundArgs A) {
         }
     }
     for (int j = tid; j < ns; j += DB_T) {
-        const int64_t t = raw[base + j];
-        s_tp[j] = (int32_t)t;
-        s_tv[j] = env[t];
+        s_tp[j] = (int32_t)raw[base + j];
+        s_tv[j] = rawv[base + j];                            /* env at the trough */
     }
     __syncthreads();
     /* staged accessors by trough index */
@@ -1179,7 +1182,7 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
     const int nu = s_nund;
     if (nu <= 0) return;                                     /* none undecided, or the full draft anyway */
     const int64_t *raw = A.raw + d0;
-    const double *env = A.env + d0;
+    const double *rawv = A.rawv + d0;                        /* env at the raw troughs */
     const int64_t W = A.window, t0 = raw[0];
     const int vf = A.vfl[2 * f], vl = A.vfl[2 * f + 1];
     auto seg_of_g = [&](int64_t x) -> int {                 /* last trough <= x, over global memory */
@@ -1201,9 +1204,8 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
         return;
     }
     for (int j = tid; j < ns; j += DB_T) {
-        const int64_t t = raw[base + j];
-        s_tp[j] = (int32_t)t;
-        s_tv[j] = env[t];
+        s_tp[j] = (int32_t)raw[base + j];
+        s_tv[j] = rawv[base + j];                            /* env at the trough */
     }
     __syncthreads();
     auto seg_of = [&](int64_t x) -> int {                   /* last trough <= x (x >= t0), among the staged */

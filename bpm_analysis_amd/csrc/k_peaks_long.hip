@@ -537,7 +537,10 @@ __global__ __launch_bounds__(1024) void k_fpl_compact(PeakArgs A, FplArgs L) {
         const bool keep = j < M && st[j] == ST_FINAL;
         int tot;
         const int off = block_scan_flag<1024>(keep, sh, &tot);
-        if (keep) out[w + off] = mp[j];
+        if (keep) {
+            out[w + off] = mp[j];
+            if (A.outv) A.outv[d0 + w + off] = A.sign * L.mh[d0 + j];
+        }
         w += tot;
     }
     if (tid == 0) {

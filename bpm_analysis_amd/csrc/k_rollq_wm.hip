@@ -157,9 +157,10 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     const int64_t xb = chunked ? t0 : 0;                     /* block table origin */
     if (fused) {
         const int64_t *tr = A.troughs + d0 + jlo;
+        const double *trv = A.tv ? A.tv + d0 + jlo : nullptr;   /* env at the troughs, beside them */
         for (int j = tid; j < ntr; j += WM_T) {
             s_tp[j] = (int32_t)tr[j];
-            s_tv[j] = A.env[d0 + tr[j]];
+            s_tv[j] = trv ? trv[j] : A.env[d0 + tr[j]];
         }
         __syncthreads();
         for (int64_t b = tid; b <= ((top - xb) >> 6); b += WM_T) {
@@ -181,7 +182,7 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
         if (!fused) {                                        /* > WM_TRMAX troughs: np.interp from global memory */
             if (!A.env) return dense[x];
             const int64_t *trg = A.troughs + d0;
-            return interp_at(x, trg, [&](int j) { return A.env[d0 + trg[j]]; }, ntr_all);
+            return interp_at(x, trg, [&](int j) { return A.tv ? A.tv[d0 + j] : A.env[d0 + trg[j]]; }, ntr_all);
         }
         const int xi = (int)x;                               /* positions < 2^31 (host check): 32-bit arithmetic */
         if (ntr == 0 || xi < s_tp[0]) return __builtin_nan("");
