@@ -266,6 +266,7 @@ static void wm_lds_attr(int device) {
     const int mx = (int)wm_layout(WM_MMAX, false).total;
     (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     (void)hipFuncSetAttribute((const void *)k_rollq_wm_t<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void *)k_floor_wm, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     done[(size_t)device] = 1;
 }
 
@@ -697,7 +698,11 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         if (bad_window)
             LAUNCH(ctx, s, "k_flag_window", k_flag_window, dim3((F + 255) / 256), dim3(256), 0, s, F, d_run1,
                    (int32_t *)O->flags);
-        if (noise_lazy) {                 /* the static-floor quantile, for recordings with < 5 troughs */
+        /* recordings of <= WM_MMAX samples: everything after the draft bracket
+         * in one launch (k_floor_wm), the static floor's quantile included */
+        const bool floor_wm = !(P->options & (BPMX_OPT_ROLLQ_MERGE | BPMX_OPT_ROLLQ_GLOBAL | BPMX_OPT_ROLLQ_NOPRUNE)) &&
+                              maxnd <= WM_MMAX;
+        if (noise_lazy && !floor_wm) {    /* the static-floor quantile, for recordings with < 5 troughs */
             QuantArgs a;
             a.env = O->env; a.doff = d_doff; a.active = d_active; a.n_files = F; a.qv = qv; a.skip_le = QR_MAX;
             a.n_levels = 1; a.q[0] = P->noise_floor_q; a.slot[0] = 1 << Q_NOISE;
@@ -864,8 +869,39 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             LAUNCH(ctx, s, "k_draft_points", k_draft_points<1>, dim3(F, gp), dim3(DB_T), 0, s, a);
             LAUNCH(ctx, s, "k_draft_points[wide]", k_draft_points<4>, dim3(F, gp), dim3(DB_T), 0, s, a);
         }
-        if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
-        {
+        SanitizeArgs sa;
+        sa.env = O->env; sa.draft = draft; sa.doff = d_doff; sa.active = d_active; sa.raw = rawt; sa.nraw = d_nraw;
+        sa.rawv = rawv; sa.outv = trv;
+        sa.n_files = F; sa.mult = P->reject_mult; sa.out = O->troughs; sa.nout = O->n_troughs; sa.flags = O->flags;
+        sa.run2 = d_run2; sa.dec = tdec; sa.exact = d_exact; sa.run_fb = d_runfb;
+        if (floor_wm) {
+            FloorWmArgs a;
+            a.rq.dense = dense; a.rq.doff = d_doff; a.rq.n_files = F; a.rq.env = O->env;
+            a.rq.window = (int32_t)W; a.rq.min_periods = P->min_periods; a.rq.cap = cap; a.rq.q = P->noise_floor_q;
+            a.rq.wm_max = WM_MMAX; a.rq.wm_chunk = 0; a.rq.wm_fail = nullptr; a.rq.wm_pos_ch = nullptr;
+            a.rq.vfirst = a.rq.vlast = nullptr; a.rq.chunk = 0; a.rq.gv = nullptr; a.rq.gp = nullptr; a.rq.gcap = 0;
+            a.rq.troughs = nullptr; a.rq.tv = nullptr; a.rq.ntr = nullptr; a.rq.run = nullptr; a.rq.out = nullptr;
+            a.rq.allnan = nullptr;
+#ifdef BPMX_STAMPS
+            a.rq.stamps = nullptr;
+#endif
+            sa.run2 = nullptr; sa.run_fb = nullptr;
+            a.sa = sa;
+            a.exact = d_exact;
+            a.qv = qv;
+            a.qn = QuantArgs{};
+            if (noise_lazy) {
+                a.qn.env = O->env; a.qn.doff = d_doff; a.qn.active = d_active; a.qn.n_files = F; a.qn.qv = qv;
+                a.qn.skip_le = QR_MAX; a.qn.n_levels = 1; a.qn.q[0] = P->noise_floor_q; a.qn.slot[0] = 1 << Q_NOISE;
+                a.qn.skip = nullptr; a.qn.stats = 0;
+            }
+            a.floor = O->floor; a.draft = draft; a.an_draft = d_an1; a.an_final = d_an2; a.full = wm_full;
+            if ((rc = rollq(d_exact, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;   /* the full draft */
+            wm_lds_attr(ctx->device);
+            LAUNCH(ctx, s, "k_floor_wm", k_floor_wm, dim3(F), dim3(WM_T), std::max(wm_lds_p, wm_lds), s, a);
+        }
+        if (!floor_wm && (rc = rollq(d_exact, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
+        if (!floor_wm) {
             SanitizeArgs a;
             a.env = O->env; a.draft = draft; a.doff = d_doff; a.active = d_active; a.raw = rawt; a.nraw = d_nraw;
             a.rawv = rawv; a.outv = trv;
@@ -873,9 +909,9 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             a.run2 = d_run2; a.dec = tdec; a.exact = d_exact; a.run_fb = d_runfb;
             LAUNCH(ctx, s, "k_sanitize", k_sanitize, dim3(F), dim3(256), 0, s, a);
         }
-        if (bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
-        if ((rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2, trv)) != BPMX_OK) return rc;
-        {
+        if (!floor_wm && bounds && (rc = rollq(d_runfb, rawt, d_nraw, draft, d_an1, rawv)) != BPMX_OK) return rc;
+        if (!floor_wm && (rc = rollq(d_run2, O->troughs, O->n_troughs, O->floor, d_an2, trv)) != BPMX_OK) return rc;
+        if (!floor_wm) {
             FinalArgs a;
             a.draft = draft; a.doff = d_doff; a.active = d_active; a.qv = qv; a.allnan_draft = d_an1;
             a.allnan_final = d_an2; a.n_files = F; a.floor = O->floor; a.flags = O->flags;

@@ -214,7 +214,7 @@ struct RollqArgs {
     int32_t *allnan;         /* [F] */
     int32_t wm_max;          /* k_rolling_quantile skips files with n <= wm_max (k_rollq_wm took them) */
     const double *env;       /* k_rollq_wm: interpolate dense from env at the troughs itself ... */
-    const double *tv;        /* ... taken from tv (env at each trough, beside troughs) when set */
+    const double *tv;        /* ... taken from tv (env at each trough, beside troughs; required with env) */
     const int32_t *ntr;      /* ... when the file has <= WM_TRMAX of them (else read dense) */
     int64_t chunk;           /* k_rolling_quantile: outputs per workgroup (blockIdx.y = chunk of the file) */
     int32_t *vfirst, *vlast; /* [F] first / last valid output over all chunks (k_rollq_fill reads them) */
@@ -250,6 +250,74 @@ struct SanitizeArgs {
     const uint8_t *dec;      /* [raw trough j at doff + j] keep decision of k_draft_bounds (nullptr: use draft) */
     const int32_t *exact;    /* [F] 1: draft computed in full, decide from it instead */
     int32_t *run_fb;         /* [F] out: draft floor kept (<= 2 troughs) but only bounded: compute it in full */
+};
+
+/* sanitize (bpm_analysis.py:1088-1099) of recording f by its NT-thread
+ * workgroup: keep raw trough t iff env[t] <= mult * draft[t] (from the draft,
+ * or from k_draft_bounds' decisions), ordered, with their env values; < 5 raw
+ * troughs: all of them, BPMX_F_STATIC_FLOOR.  Returns the kept count to every
+ * thread.  k_sanitize, and k_floor_wm's workgroups (k_rollq_wm.hip). */
+template <int NT>
+__device__ __forceinline__ int sanitize_wg(const SanitizeArgs &A, int f, int *sh) {
+    const int64_t d0 = A.doff[f];
+    const int64_t *raw = A.raw + d0;
+    int64_t *out = A.out + d0;
+    const int m = A.nraw[f];
+    const int tid = threadIdx.x;
+    const double *rawv = A.rawv + d0;
+    double *outv = A.outv + d0;
+    if (m < 5) {
+        for (int j = tid; j < m; j += NT) { out[j] = raw[j]; outv[j] = rawv[j]; }
+        if (tid == 0) {
+            A.nout[f] = m;
+            A.flags[f] |= BPMX_F_STATIC_FLOOR;
+            if (A.run2) A.run2[f] = 0;
+        }
+        return m;
+    }
+    const double *draft = A.draft + d0;
+    const bool exact = !A.dec || A.exact[f];
+    int w = 0;
+    for (int c0 = 0; c0 < m; c0 += NT) {
+        const int j = c0 + tid;
+        bool keep = false;
+        int64_t t = 0;
+        double tv = 0.0;
+        if (j < m) {
+            t = raw[j];
+            tv = rawv[j];                                    /* env[t] */
+            if (exact) {
+                const double fl = draft[t];
+                keep = (fl == fl) && tv <= A.mult * fl;
+            } else {
+                keep = A.dec[d0 + j] == 1;
+            }
+        }
+        int tot;
+        const int off = block_scan_flag<NT>(keep, sh, &tot);
+        if (keep) { out[w + off] = t; outv[w + off] = tv; }
+        w += tot;
+    }
+    if (tid == 0) {
+        A.nout[f] = w;
+        if (w <= 2) A.flags[f] |= BPMX_F_DRAFT_FLOOR;
+        if (A.run2) A.run2[f] = w > 2 ? 1 : 0;
+        if (A.run_fb) A.run_fb[f] = (w <= 2 && !exact) ? 1 : 0;
+    }
+    return w;
+}
+
+/* k_floor_wm (k_rollq_wm.hip): the floor stage after the draft bracket in one
+ * workgroup per recording (recordings of <= WM_MMAX decimated samples) */
+struct FloorWmArgs {
+    RollqArgs rq;              /* the rolling-quantile settings; troughs / tv / ntr / out / allnan / run set per call */
+    SanitizeArgs sa;           /* raw troughs and values, draft, decisions -> kept troughs, values, counts, flags */
+    const int32_t *exact;      /* [F] the draft floor in full here (the bracket left it open) */
+    const double *qv;          /* [F][Q_SLOTS] */
+    QuantArgs qn;              /* n_levels 1: the static floor's level, selected here (lazy); 0: in qv already */
+    double *floor, *draft;     /* draft: the same buffer as sa.draft */
+    int32_t *an_draft, *an_final;   /* [F] all-NaN results of the draft / final rolling quantiles */
+    int32_t *full;             /* [F] scratch of the pruned / unpruned decision */
 };
 
 /* k_draft_bounds: the draft floor (first rolling quantile) is read only at the
@@ -381,6 +449,7 @@ __host__ __device__ inline WmLayout wm_layout(int64_t nmax, bool prune) {
 }
 template <bool PRUNE>
 __global__ void k_rollq_wm_t(RollqArgs A, uint16_t *pos_scratch, int32_t *full);
+__global__ void k_floor_wm(FloorWmArgs A);
 
 }  // namespace bpmx
 

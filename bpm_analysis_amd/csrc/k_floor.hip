@@ -612,50 +612,9 @@ template __global__ void k_rolling_quantile<256, 32>(RollqArgs A);
 
 /* ------------------------------------------------------------------------ */
 __global__ __launch_bounds__(256) void k_sanitize(SanitizeArgs A) {
-    const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f]) return;
     __shared__ int sh[256 / 64 + 1];
-    const int64_t d0 = A.doff[f];
-    const int64_t *raw = A.raw + d0;
-    int64_t *out = A.out + d0;
-    const int m = A.nraw[f];
-    const int tid = threadIdx.x;
-    const double *rawv = A.rawv + d0;
-    double *outv = A.outv + d0;
-    if (m < 5) {
-        for (int j = tid; j < m; j += 256) { out[j] = raw[j]; outv[j] = rawv[j]; }
-        if (tid == 0) { A.nout[f] = m; A.flags[f] |= BPMX_F_STATIC_FLOOR; A.run2[f] = 0; }
-        return;
-    }
-    const double *draft = A.draft + d0;
-    const bool exact = !A.dec || A.exact[f];
-    int w = 0;
-    for (int c0 = 0; c0 < m; c0 += 256) {
-        const int j = c0 + tid;
-        bool keep = false;
-        int64_t t = 0;
-        double tv = 0.0;
-        if (j < m) {
-            t = raw[j];
-            tv = rawv[j];                                    /* env[t] */
-            if (exact) {
-                const double fl = draft[t];
-                keep = (fl == fl) && tv <= A.mult * fl;
-            } else {
-                keep = A.dec[d0 + j] == 1;
-            }
-        }
-        int tot;
-        const int off = block_scan_flag<256>(keep, sh, &tot);
-        if (keep) { out[w + off] = t; outv[w + off] = tv; }
-        w += tot;
-    }
-    if (tid == 0) {
-        A.nout[f] = w;
-        if (w <= 2) A.flags[f] |= BPMX_F_DRAFT_FLOOR;
-        A.run2[f] = w > 2 ? 1 : 0;
-        if (A.run_fb) A.run_fb[f] = (w <= 2 && !exact) ? 1 : 0;
-    }
+    const int f = blockIdx.x;
+    if (f < A.n_files && A.active[f]) (void)sanitize_wg<256>(A, f, sh);
 }
 
 /* ------------------------------------------------------------------------ */

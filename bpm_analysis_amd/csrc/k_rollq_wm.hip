@@ -46,6 +46,7 @@
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 #include "bpmx_stamps.h"
+#include "bpmx_qsel.h"
 
 namespace bpmx {
 
@@ -157,10 +158,10 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     const int64_t xb = chunked ? t0 : 0;                     /* block table origin */
     if (fused) {
         const int64_t *tr = A.troughs + d0 + jlo;
-        const double *trv = A.tv ? A.tv + d0 + jlo : nullptr;   /* env at the troughs, beside them */
+        const double *trv = A.tv + d0 + jlo;                 /* env at the troughs, beside them */
         for (int j = tid; j < ntr; j += WM_T) {
             s_tp[j] = (int32_t)tr[j];
-            s_tv[j] = trv ? trv[j] : A.env[d0 + tr[j]];
+            s_tv[j] = trv[j];
         }
         __syncthreads();
         for (int64_t b = tid; b <= ((top - xb) >> 6); b += WM_T) {
@@ -182,7 +183,7 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
         if (!fused) {                                        /* > WM_TRMAX troughs: np.interp from global memory */
             if (!A.env) return dense[x];
             const int64_t *trg = A.troughs + d0;
-            return interp_at(x, trg, [&](int j) { return A.tv ? A.tv[d0 + j] : A.env[d0 + trg[j]]; }, ntr_all);
+            return interp_at(x, trg, [&](int j) { return A.tv[d0 + j]; }, ntr_all);
         }
         const int xi = (int)x;                               /* positions < 2^31 (host check): 32-bit arithmetic */
         if (ntr == 0 || xi < s_tp[0]) return __builtin_nan("");
@@ -937,5 +938,87 @@ __global__ __launch_bounds__(WM_T) void k_rollq_wm_t(RollqArgs A, uint16_t *pos_
 
 template __global__ void k_rollq_wm_t<true>(RollqArgs, uint16_t *, int32_t *);
 template __global__ void k_rollq_wm_t<false>(RollqArgs, uint16_t *, int32_t *);
+
+/* one rolling quantile of recording blockIdx.x: pruned, or unpruned in the
+ * same workgroup when the pruned structure cannot take it */
+__device__ __forceinline__ void rollq_wm_run(const RollqArgs &a, int32_t *full, RqShared &sh) {
+    if (rollq_wm_body<true>(a, nullptr, full, sh)) {
+        __syncthreads();
+        (void)rollq_wm_body<false>(a, nullptr, full, sh);
+    }
+}
+
+/* ---------------------------------------------------------------------------
+ * k_floor_wm: the noise floor after the draft, one workgroup per recording
+ * (bpm_analysis.py:1088-1117, recordings of at most WM_MMAX decimated
+ * samples): sanitize (sanitize_wg) from k_draft_bounds' / k_draft_points'
+ * decisions or the full draft; then < 5 raw troughs: the static floor,
+ * quantile(env, noise_floor_q), selected here when no earlier stage selected
+ * it (qn, the lazy level); > 2 kept troughs: the final rolling quantile; else
+ * the draft floor (the full draft when it was computed, else its rolling
+ * quantile here); an all-NaN floor: quantile(env, 0.1).  One launch for what
+ * took k_sanitize, k_rollq_wm_t (draft fallback), k_rollq_wm_t (final),
+ * k_floor_final and the lazy k_quantile_reg, with no device round trip of the
+ * per-recording decisions.  (The full draft before sanitize stays a launch of
+ * its own: a second rolling-quantile call site in this kernel spills.)
+ * ------------------------------------------------------------------------- */
+__global__ __launch_bounds__(WM_T) void k_floor_wm(FloorWmArgs A) {
+    __shared__ RqShared sh;
+    __shared__ int s_sc[WM_T / 64 + 1];
+    extern __shared__ __align__(16) unsigned char smem[];
+    const RollqArgs &R = A.rq;
+    const int f = blockIdx.x;
+    if (f >= R.n_files || !A.sa.active[f]) return;
+    const int64_t d0 = R.doff[f], n = R.doff[f + 1] - d0;
+    const int m = A.sa.nraw[f], tid = threadIdx.x;
+    const bool have_draft = m >= 5 && A.exact[f];            /* the full draft, computed before */
+    const int w = __builtin_amdgcn_readfirstlane(sanitize_wg<WM_T>(A.sa, f, s_sc));   /* uniform */
+    __syncthreads();
+    const bool final = m >= 5 && w > 2;
+    if (m >= 5 && (final || !have_draft)) {                 /* the final floor, or the draft floor here */
+        RollqArgs a = R;
+        a.troughs = final ? A.sa.out : A.sa.raw;
+        a.tv = final ? A.sa.outv : A.sa.rawv;
+        a.ntr = final ? A.sa.nout : A.sa.nraw;
+        a.allnan = final ? A.an_final : A.an_draft;
+        a.out = A.floor;
+        a.run = A.sa.active;                                 /* (1 here) */
+        rollq_wm_run(a, A.full, sh);
+        __syncthreads();
+    }
+    bool fill = false, from_draft = false, nanfb = false;
+    double v = 0.0;
+    const double *qv = A.qv + (int64_t)f * Q_SLOTS;
+    if (m < 5) {                                             /* static floor */
+        if (A.qn.n_levels > 0) {
+            const double *x = R.env + d0;
+            uint64_t key[QR_IT];
+#pragma unroll
+            for (int it = 0; it < QR_IT; ++it) {
+                const int64_t i = (int64_t)it * QR_T + tid;
+                key[it] = i < n ? f64_key(x[i]) : 0ull;
+            }
+            qr_select(key, n, A.qn, f, *reinterpret_cast<QrShared *>(smem));
+            __syncthreads();
+        }
+        v = qv[Q_NOISE];
+        fill = true;
+    } else if (final) {
+        nanfb = A.an_final[f] != 0;
+    } else {
+        from_draft = have_draft;
+        nanfb = A.an_draft[f] != 0;
+    }
+    if (nanfb) {
+        fill = true;
+        from_draft = false;
+        v = qv[Q_FALLBACK];
+    }
+    double *floor = A.floor + d0;
+    const double *draft = A.draft + d0;
+    if (fill || from_draft)
+        for (int64_t i = tid; i < n; i += WM_T) floor[i] = from_draft ? draft[i] : v;
+    if (tid == 0 && nanfb) A.sa.flags[f] |= BPMX_F_NAN_FLOOR;
+}
 
 }  // namespace bpmx

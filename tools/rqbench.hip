@@ -66,7 +66,15 @@ int main(int argc, char **argv) {
     a.min_periods = 3; a.cap = 0; a.q = 0.2; a.out = d_out; a.allnan = d_an; a.stamps = d_st;
     a.wm_max = WM_MMAX; a.env = d_env; a.ntr = d_ntr; a.wm_chunk = 0; a.wm_fail = nullptr; a.wm_pos_ch = nullptr;
     a.vfirst = a.vlast = nullptr;
-    a.tv = nullptr;
+    {   /* env at each trough, beside the troughs (the library's trough values) */
+        std::vector<double> tvh(N, 0.0);
+        for (int f = 0; f < F; ++f)
+            for (int j = 0; j < ntr[f]; ++j) tvh[(size_t)f * nd + j] = env[(size_t)f * nd + tr[(size_t)f * nd + j]];
+        double *d_tv;
+        CK(hipMalloc(&d_tv, N * 8));
+        CK(hipMemcpy(d_tv, tvh.data(), N * 8, hipMemcpyHostToDevice));
+        a.tv = d_tv;
+    }
     const size_t lds = std::max(wm_layout(nd, true).total, wm_layout(nd, false).total);   /* the unpruned fallback runs in the same workgroup */
     CK(hipFuncSetAttribute((const void *)k_rollq_wm_t<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t e0, e1;
