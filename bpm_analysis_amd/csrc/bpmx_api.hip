@@ -31,6 +31,8 @@
 #include "bpmx_fpscan.h"
 #include "bpmx_synth.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 using namespace bpmx;
 
 namespace bpmx {
@@ -42,6 +44,19 @@ int fail(int code, const std::string &msg) {
 }  // namespace bpmx
 
 namespace {
+
+/* Per-stage roctx ranges (SURVEY.md §5 tracing): a run's ENVELOPE, FLOOR and
+ * PEAKS launches are enqueued inside "bpmx:<stage>" ranges, so a profile taken
+ * with rocprofv3 --marker-trace --kernel-trace groups each kernel under its
+ * stage (the reference itself only logs a total time, bpm_analysis.py:1727,
+ * :1767-1768).  The ranges cover host-side enqueueing; the kernels they
+ * correlate with run asynchronously after. */
+struct StageRange {
+    explicit StageRange(const char *name) { roctxRangePushA(name); }
+    ~StageRange() { roctxRangePop(); }
+    StageRange(const StageRange &) = delete;
+    StageRange &operator=(const StageRange &) = delete;
+};
 
 /* per-run output init from the cached device geometry (no pageable H2D copy
  * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
@@ -428,6 +443,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     }
     bool q_in_env = false;                /* every active recording's quantiles came with its envelope */
     if (do_env) {
+        StageRange range("bpmx:envelope");
         if (P->mode == BPMX_MODE_REFERENCE) {
             double *scr = (double *)ctx->buf("ref_scratch", (size_t)((maxnd + 30 + 63) / 64 * 64) * F * 8, &rc);
             if (rc != BPMX_OK) return rc;
@@ -565,6 +581,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     if (!do_floor && !do_peaks) return BPMX_OK;
 
     /* ---- shared detection inputs: block tables, quantiles ---- */
+    StageRange range_in("bpmx:detection-inputs");
     double *bmax = (double *)ctx->buf("bmax", (size_t)sumb * 8, &rc);
     double *bmin = (double *)ctx->buf("bmin", (size_t)sumb * 8, &rc);
     int32_t *fp_fb = (int32_t *)ctx->buf("fp_fallback", (size_t)F * 4, &rc);
@@ -676,6 +693,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
 
     /* ---- FLOOR ---- */
     if (do_floor) {
+        StageRange range("bpmx:floor");
         int64_t *rawt = (int64_t *)ctx->buf("raw_troughs", (size_t)sumnd * 8, &rc);
         /* env at the raw and at the sanitised troughs, beside the indices (the
          * trough search and k_sanitize write them; the floor kernels read them
@@ -928,6 +946,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
 
     /* ---- PEAKS ---- */
     if (do_peaks) {
+        StageRange range("bpmx:peaks");
         PeakArgs a;
         a.env = O->env; a.height = O->floor; a.doff = d_doff; a.boff = d_boff; a.active = d_active;
         a.bmax = bmax; a.bmin = bmin; a.qv = qv; a.qslot = Q_PEAK; a.n_files = F; a.distance = P->distance;

@@ -142,6 +142,12 @@ __device__ __forceinline__ V4 mv_rot(const double *r, const V4 &x) {
               __builtin_fma(a2, x.d, -b2 * x.c)};
 }
 __device__ __forceinline__ V4 add4(const V4 &x, const V4 &y) { return V4{x.a + y.a, x.b + y.b, x.c + y.c, x.d + y.d}; }
+/* acc + rot(r) x with the sum folded into the rotation's FMAs (two per component) */
+__device__ __forceinline__ V4 acc_rot(const V4 &acc, const double *r, const V4 &x) {
+    const double a1 = r[0], b1 = r[1], a2 = r[2], b2 = r[3];
+    return V4{__builtin_fma(a1, x.a, __builtin_fma(b1, x.b, acc.a)), __builtin_fma(a1, x.b, __builtin_fma(-b1, x.a, acc.b)),
+              __builtin_fma(a2, x.c, __builtin_fma(b2, x.d, acc.c)), __builtin_fma(a2, x.d, __builtin_fma(-b2, x.c, acc.d))};
+}
 __device__ __forceinline__ M4 mm(const M4 &X, const M4 &Y) {
     M4 R;
 #pragma unroll
@@ -284,7 +290,7 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const d
 #define NAT_UP(K)                                                            \
     {                                                                        \
         const V4 y = K == 0 ? xl_up_v<1>(incl) : shfl_up_v(incl, 1 << K);   \
-        if (lane >= (1 << K)) incl = add4(incl, mv_rot(et + ET_KPOW + 4 * K, y)); \
+        if (lane >= (1 << K)) incl = acc_rot(incl, et + ET_KPOW + 4 * K, y);   \
     }
     NAT_UP(0) NAT_UP(1) NAT_UP(2) NAT_UP(3) NAT_UP(4) NAT_UP(5)
 #undef NAT_UP
@@ -295,7 +301,7 @@ __device__ __forceinline__ void nat_tile_epilogue(const NatBlockArgs &A, const d
 #define NAT_DOWN(K)                                                          \
     {                                                                        \
         const V4 y = K == 0 ? xl_down_v<1>(R) : shfl_down_v(R, 1 << K);      \
-        if (lane + (1 << K) < 64) R = add4(R, mv_rot(et + ET_KPOW + 4 * K, y)); \
+        if (lane + (1 << K) < 64) R = acc_rot(R, et + ET_KPOW + 4 * K, y);     \
     }
     NAT_DOWN(0) NAT_DOWN(1) NAT_DOWN(2) NAT_DOWN(3) NAT_DOWN(4) NAT_DOWN(5)
 #undef NAT_DOWN
@@ -603,6 +609,9 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
             const int hw0 = coff + (b < Lt ? b : 0) * ds + 16 * hf;      /* halfword index of k-group start */
             const uint32_t sh = (hw0 & 1) ? 16u : 0u;
             nm_i16 acc0 = s_init[hf], acc1 = s_init[2 + hf];
+#ifdef BPMX_NM_NOMFMA                                         /* timing diagnostic: no matrix phase (wrong outputs) */
+            acc0[0] += (int)tw[hw0 >> 1];
+#else
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const uint32_t *p = tw + ((hw0 + 32 * s) >> 1);
@@ -622,6 +631,7 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
                 acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0][s][1], bh, acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1][s][1], bh, acc1, 0, 0, 0);
             }
+#endif
             /* |acc| <= 2*160*128*128 + 128*147*128 < 2^23, so a row pair
              * a_r + 256 a_(r+1) fits int32; two pairs combine exactly in f64
              * (< 2^48), and H 2^32 + L is the one rounding. */
@@ -650,8 +660,12 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
             cf[2 * q] = hf ? other : res[0][q];
             cf[2 * q + 1] = hf ? res[1][q] : other;
         }
+#ifdef BPMX_NM_NOEPI                                          /* timing diagnostic: no epilogue (wrong outputs) */
+        if (cf[0] == 1.2345e300 && cf[7] == x0) A.gam[0] = cf[3];
+#else
         nat_tile_epilogue(A, s_et, tl, t, lane, valid, V4{cf[0], cf[1], cf[2], cf[3]}, V4{cf[4], cf[5], cf[6], cf[7]},
                           x0);
+#endif
         if (NM_SLOTS == 1) tl = tn;
         else if (t + stride < A.n_tiles) tl = nat_tile_ld(A.tiles, t + stride);
     }
