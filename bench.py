@@ -85,11 +85,15 @@ def parse(argv=None):
     ap.add_argument("--undecided-mult", type=float, default=1.0,
                     help="side measurement: the step with trough_rejection_multiplier set to this, which leaves "
                          "many troughs inside the draft-floor bracket (decided by draft_point); 0: skip")
+    ap.add_argument("--real-env-steps", type=int, default=5,
+                    help="side measurement: the detection stages (noise floor + raw peaks) on 60 s windows of a "
+                         "real recording's envelope (the reference's vulpine sample, tests/golden) beside the "
+                         "same stages on the synthetic batch's envelopes (0: skip)")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="TESTS ONLY: oracle-backed detector (tests/bench_stub.py) over gloo on CPU ranks")
     a = ap.parse_args(argv)
     if a.cpu_stub:          # the side measurements need device memory and streams
-        a.pcie_steps = a.contexts = a.exact_steps = a.dropin_files = 0
+        a.pcie_steps = a.contexts = a.exact_steps = a.dropin_files = a.real_env_steps = 0
         a.undecided_mult = 0.0
         a.c5_contexts = 1
     return a
@@ -750,6 +754,86 @@ def main(args):
                      **res}
         del base
 
+    # Side measurement (never `value`): the detection stages on REAL envelopes.
+    # The synthetic generator's recordings leave no trough inside the draft
+    # bracket and prune well; a real recording does neither as well.  Two
+    # envelopes of the reference's own vulpine sample (tests/golden/vulpine.npz,
+    # 377 s at 302 Hz): "reference" = its reference-pipeline envelope (rolling
+    # mean of |filtfilt|, the 20-150 Hz ripple kept), "native_style" =
+    # rolling mean of |hilbert| of its filtered, decimated signal (the sample
+    # WAV itself), i.e. what native mode computes, made on the host as input.
+    # Each is cut into F windows of the batch's decimated length at spread
+    # offsets; FLOOR | PEAKS run on them and, for comparison, on the timed
+    # batch's synthetic envelopes.  Recordings with a decisive tie are counted
+    # and re-decided in numpy's order (engine.resolve_ties), timed apart; a
+    # sample of windows is checked against the numpy-order oracle.
+    real = None
+    if rank == 0 and args.real_env_steps > 0 and args.mode == "native":
+        import pandas as pd
+        import scipy.signal as ssig
+        from bpm_analysis_amd import _native as N
+        from bpm_analysis_amd.design import detect_design
+        g = np.load(os.path.join(REPO, "tests", "golden", "vulpine.npz"), allow_pickle=False)
+        sr = int(g["sr"])
+        if sr == d.sr and len(g["env"]) > nd:
+            sources = {
+                "reference": np.ascontiguousarray(g["env"], dtype=np.float64),
+                "native_style": pd.Series(np.abs(ssig.hilbert(g["pcm"].astype(np.float64)))).rolling(
+                    sr // 10, min_periods=1, center=True).mean().to_numpy(),
+            }
+            fr = np.arange(F + 1, dtype=np.int64) * nd
+            dr = detect_design(sr, params)
+            st = N.STAGE_FLOOR | N.STAGE_PEAKS
+            out_d = det.alloc(fr, 1, sr)
+
+            def det_time(o):
+                det.run(None, fr, sr, params, stages=st, out=o, d=dr, options=args.options)
+                torch.cuda.synchronize()
+                tr0 = time.perf_counter()
+                for _ in range(args.real_env_steps):
+                    det.run(None, fr, sr, params, stages=st, out=o, d=dr, options=args.options)
+                torch.cuda.synchronize()
+                return (time.perf_counter() - tr0) / args.real_env_steps * 1e3
+
+            out_d.env.copy_(out.env)
+            real = {"recordings": F, "samples_per_recording": nd, "sr": sr, "steps": args.real_env_steps,
+                    "stages": "FLOOR | PEAKS (noise floor, troughs, raw peaks)",
+                    "windows": "offsets (k * 997) mod (len - Nd), k < recordings",
+                    "synthetic_envelopes_ms_per_batch": det_time(out_d)}
+            from oracle import oracle as O
+            od = O.derive(fs, params)
+            for name, env0 in sources.items():
+                starts = [(k * 997) % (len(env0) - nd) for k in range(F)]
+                out_d.env.copy_(torch.from_numpy(np.concatenate([env0[s0:s0 + nd] for s0 in starts])).to(det.device))
+                ms_r = det_time(out_d)
+                det.run(None, fr, sr, params, stages=st, out=out_d, d=dr, options=args.options | N.OPT_STATS)
+                stt = det.stats()
+                fl = out_d.flags.cpu().numpy()
+                n_tie = int(np.count_nonzero(fl & (N.F_TROUGH_TIE | N.F_PEAK_TIE)))
+                torch.cuda.synchronize()
+                tt0 = time.perf_counter()
+                n_res = det.resolve_ties(out_d, params, st)
+                torch.cuda.synchronize()
+                t_res = (time.perf_counter() - tt0) * 1e3
+                rhost = out_d.to_host()
+                pick = sorted(set(np.linspace(0, F - 1, min(F, 8)).astype(int).tolist()))
+                ok = 0
+                for k in pick:
+                    e = np.ascontiguousarray(env0[starts[k]:starts[k] + nd])
+                    of, ot, ofl, _ = O.noise_floor_numpy_order(e, od, params)
+                    opk = O.find_peaks_numpy_order(e, height=of, distance=od.distance,
+                                                   prominence=O.quantile(e, params["peak_prominence_quantile"]))
+                    r = rhost[k]
+                    ok += int(np.array_equal(r["troughs"], ot) and np.array_equal(r["peaks"], opk) and
+                              np.array_equal(r["floor"], of, equal_nan=True) and (r["flags"] & 7) == (ofl & 7))
+                real[name] = {"ms_per_batch": ms_r, "raw_troughs": stt["raw_troughs"],
+                              "undecided_troughs": stt["undecided"],
+                              "undecided_frac": stt["undecided"] / max(1, stt["raw_troughs"]),
+                              "full_draft_chunks": stt["full_draft_chunks"], "tie_flagged_recordings": n_tie,
+                              "ties_resolved": n_res, "tie_resolution_ms": t_res,
+                              "parity": {"files": len(pick), "equal_to_numpy_order_oracle": ok}}
+            del out_d
+
     # Parity of the timed batch against the oracle on the same recordings.  N = 1:
     # every file, in the cpu_baseline leg below.  N > 1: a bounded sample of
     # every rank's shard, counts summed over ranks; rank 0's sample, timed on
@@ -894,6 +978,7 @@ def main(args):
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,
             "result_gather": gathered, "multi_context": multi, "exact_no_shortcuts": exact,
             "host_beat_stages": host_beats, "dropin_latency": dropin, "draft_undecided": undecided,
+            "real_envelope_detection": real,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
