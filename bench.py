@@ -165,9 +165,12 @@ def algorithmic_bytes_total(mode: str, F: int, frames: int, nd: int, channels: i
         "k_find_peaks[troughs]": nd * 8,
         "k_find_peaks[peaks]": nd * 16,                # env + floor
         "k_draft_bounds": nd // 76 * 16,               # ~1 raw trough per 76 samples x (position, value)
-        # final floor: dense (interpolated in-kernel from the troughs) in, floor out; the
-        # draft pass runs only for recordings with an undecided trough (none on this workload)
-        "k_rollq_wm": nd * 8,
+        # the noise floor after the draft bracket (k_floor_wm: sanitize, the final rolling
+        # quantile interpolated in-kernel from the kept troughs' values, the fallbacks): floor
+        # out; the full-draft pass (k_rollq_wm) runs only for recordings whose bracket stayed
+        # open past draft_point (none on this workload)
+        "k_floor_wm": nd * 8,
+        "k_rollq_wm": 0,
         "k_rollq_wm[full]": 0,                          # unpruned variant: recordings the pruned one flags (none here)
         "k_init_out": 0,
         "k_rolling_quantile": nd * 16,

@@ -65,7 +65,7 @@ def test_algorithmic_bytes_native_reads_pcm_once():
     import bench
     ab = bench.algorithmic_bytes("native", 1024, 2646000, 18124, 146)
     assert ab["k_native_blocks"] == 1024 * 2646000 * 2
-    assert set(ab) >= {"k_rollq_wm", "k_native_carry", "k_hilbert_env", "k_find_peaks[peaks]"}
+    assert set(ab) >= {"k_floor_wm", "k_rollq_wm", "k_native_carry", "k_hilbert_env", "k_find_peaks[peaks]"}
 
 
 def _lpt_worker(rank, world, port, q):

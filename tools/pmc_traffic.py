@@ -38,7 +38,7 @@ def short_name(kernel: str) -> str:
 # (bpmx_api.hip's LAUNCH names), in launch order within a step: their
 # dispatches are labelled by their position in that cycle
 LABEL_CYCLE = {"k_find_peaks_lds": ["k_find_peaks[troughs]", "k_find_peaks[peaks]"],
-               "k_rollq_wm_t": ["k_rollq_wm[draft]", "k_rollq_wm[draft-fallback]", "k_rollq_wm[final]"]}
+               "k_rollq_wm_t": ["k_rollq_wm[draft]"]}      # r05: the floor's other passes are k_floor_wm
 
 
 def per_kernel(d: str, counter: str) -> dict:
@@ -64,7 +64,7 @@ def per_kernel(d: str, counter: str) -> dict:
 # measures FETCH_SIZE against known bytes per width; 16: LDS-DMA / dwordx4)
 READ_WIDTH = {"k_native_blocks_mfma": 16, "k_native_blocks_dma": 16, "k_native_blocks_i16": 16,
               "k_find_peaks_lds": 8, "k_find_peaks": 8, "k_hilbert_env": 8, "k_native_yd": 8,
-              "k_quantile_reg": 8, "k_rollq_wm_t": 8, "k_draft_bounds": 8, "k_native_carry": 8}
+              "k_quantile_reg": 8, "k_rollq_wm_t": 8, "k_floor_wm": 8, "k_draft_bounds": 8, "k_native_carry": 8}
 
 
 def calibration(fetch_dir: str, write_dir: str, nbytes: int = 768 << 20) -> dict:
