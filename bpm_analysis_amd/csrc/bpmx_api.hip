@@ -60,19 +60,9 @@ struct StageRange {
 
 /* per-run output init from the cached device geometry (no pageable H2D copy
  * on the run path): flags = TOO_SHORT for inactive recordings, counts 0 */
-__global__ __launch_bounds__(256) void k_init_out(int n_files, const int32_t *active, int32_t *flags, int32_t *ntr,
-                                                  int32_t *npk, int32_t *runs, int32_t *nraw, int32_t *z1,
-                                                  int32_t *z2, int32_t *z3) {
+__global__ __launch_bounds__(256) void k_init_out(InitOutArgs I) {
     const int f = blockIdx.x * 256 + threadIdx.x;
-    if (f >= n_files) return;
-    flags[f] = active[f] ? 0 : BPMX_F_TOO_SHORT;
-    if (ntr) ntr[f] = 0;
-    if (npk) npk[f] = 0;
-    for (int k = 0; k < 5; ++k) runs[(int64_t)k * n_files + f] = 0;
-    if (nraw) nraw[f] = 0;                                   /* the caller's raw-trough counts */
-    if (z1) z1[f] = 0;                                       /* draft exact masks (one int per recording) */
-    if (z2) { z2[f] = 0; z2[n_files + f] = 0; }              /* draft undecided counters nund[f], nund[F + f] */
-    if (z3) z3[f] = 0;                                       /* find_peaks' scan record: none yet in this run */
+    if (f < I.n_files) init_out_one(I, f);
 }
 
 /* recordings with >= 5 raw troughs reach the rolling quantile: with a noise
@@ -407,9 +397,16 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         fp_scan = (int32_t *)ctx->buf("fp_scan", (size_t)F * 4 * (1 + 2 * FPS_NW), &rc);
         if (rc != BPMX_OK) return rc;
     }
-    LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, F, d_active, (int32_t *)O->flags,
-           do_floor ? (int32_t *)O->n_troughs : nullptr, do_peaks ? (int32_t *)O->n_peaks : nullptr, d_run1,
-           d_nraw != di + 5 * F ? d_nraw : nullptr, draft_masks, bounds ? draft_vfl + 2 * F : nullptr, fp_scan);
+    InitOutArgs io;
+    io.active = d_active; io.flags = (int32_t *)O->flags; io.n_files = F;
+    io.ntr = do_floor ? (int32_t *)O->n_troughs : nullptr;
+    io.npk = do_peaks ? (int32_t *)O->n_peaks : nullptr;
+    io.runs = d_run1;
+    io.nraw = d_nraw != di + 5 * F ? d_nraw : nullptr;       /* the caller's raw-trough counts */
+    io.z1 = draft_masks; io.z2 = bounds ? draft_vfl + 2 * F : nullptr; io.z3 = fp_scan;
+    /* a native envelope stage resets them in k_native_carry (one launch fewer) */
+    const bool init_in_carry = do_env && P->mode != BPMX_MODE_REFERENCE;
+    if (!init_in_carry) LAUNCH(ctx, s, "k_init_out", k_init_out, dim3((F + 255) / 256), dim3(256), 0, s, io);
 
     /* ---- ENVELOPE ---- */
     /* the detection stage's quantile levels, built here so that the fused
@@ -570,7 +567,7 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             }
         } else {
             int r = native_envelope(ctx, P, B, O, s, F, foff, doff, maxnd, d_foff, d_doff, d_active,
-                                    (do_floor || do_peaks) ? &qa : nullptr);
+                                    (do_floor || do_peaks) ? &qa : nullptr, &io);
             if (r != BPMX_OK) return r;
             if (do_floor || do_peaks) {
                 q_in_env = true;

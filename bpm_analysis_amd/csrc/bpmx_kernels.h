@@ -11,6 +11,30 @@ namespace bpmx {
 /* per-file quantile slots in the qv[F][4] table */
 enum { Q_TROUGH = 0, Q_PEAK = 1, Q_NOISE = 2, Q_FALLBACK = 3, Q_SLOTS = 4 };
 
+/* A run's per-recording outputs and counters, reset before its stages: by
+ * k_init_out, or (native runs with an envelope stage) by k_native_carry's
+ * workgroup for its recording, which saves that launch.  Null pointers are
+ * skipped; flags == null: nothing to do. */
+struct InitOutArgs {
+    const int32_t *active;
+    int32_t *flags, *ntr, *npk, *runs, *nraw;
+    int32_t *z1;           /* draft exact masks (one int per recording) */
+    int32_t *z2;           /* draft undecided counters nund[f], nund[F + f] */
+    int32_t *z3;           /* find_peaks' scan record: none yet in this run */
+    int32_t n_files;
+};
+__device__ __forceinline__ void init_out_one(const InitOutArgs &I, int f) {
+    const int F = I.n_files;
+    I.flags[f] = I.active[f] ? 0 : BPMX_F_TOO_SHORT;
+    if (I.ntr) I.ntr[f] = 0;
+    if (I.npk) I.npk[f] = 0;
+    for (int k = 0; k < 5; ++k) I.runs[(int64_t)k * F + f] = 0;
+    if (I.nraw) I.nraw[f] = 0;
+    if (I.z1) I.z1[f] = 0;
+    if (I.z2) { I.z2[f] = 0; I.z2[F + f] = 0; }
+    if (I.z3) I.z3[f] = 0;
+}
+
 struct EnvRefArgs {
     const void *pcm;
     const int64_t *foff;   /* [F+1] frame offsets */

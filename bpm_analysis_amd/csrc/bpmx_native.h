@@ -13,7 +13,8 @@ namespace bpmx {
 int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
                     const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active,
-                    const QuantArgs *qa = nullptr);   /* non-null: the fused Hilbert kernel also fills qa->qv */
+                    const QuantArgs *qa = nullptr,    /* non-null: the fused Hilbert kernel also fills qa->qv */
+                    const InitOutArgs *io = nullptr); /* non-null: k_native_carry resets the run's outputs */
 /* k_bluestein.hip: hb = N * Hilbert transform of yd for the listed recordings */
 /* rocfft_setup() exactly once per process (std::call_once), whatever thread gets there first */
 int rocfft_setup_once();

@@ -64,7 +64,7 @@ constexpr int NAT_DSMAX = 1280;       /* decimation factors up to fs/300 - 1 at 
 
 struct NatTile {
     int64_t s0;                         /* first frame of the tile (index into pcm frames) */
-    int64_t gbase;                      /* boff[f] + j0: gamma index of the tile's first block */
+    int64_t gbase;                      /* tile index * gstr: the tile's gamma row (128-byte aligned) */
     int64_t ybase;                      /* doff[f] + j0: yd index of the tile's first block */
     int32_t j0, nb;                     /* first block, blocks of the file */
     int32_t f, pad;
@@ -88,7 +88,7 @@ struct NatBlockArgs {
     int64_t n_tiles, total;       /* tiles; samples in pcm (int16 path) */
     int32_t bt, channels, ds;     /* blocks per (full) tile */
     const double *tab, *tt;       /* block tables; tile tables */
-    double *gam;                  /* [sum blocks] */
+    double *gam;                  /* [n_tiles][gstr]: one aligned row per tile */
     double *agg;                  /* [n_tiles][8]: forward tile sum, backward R_0 */
     double *part;                 /* [F][64][NAT_PART]: raw blocks of each file's partial last tile */
 };
@@ -102,6 +102,7 @@ struct NatCarryArgs {
     double *part;                  /* partial-tile blocks; k_native_carry adds their states */
     double *carry;                 /* [n_tiles][8]: S0_t, Qe_t */
     double *yd;
+    InitOutArgs io;                /* io.flags non-null: reset recording f's outputs first */
 };
 
 struct NatYdArgs {
@@ -1069,7 +1070,9 @@ __device__ __forceinline__ Cx2 shfl_down_cx2(const Cx2 &x, int d) {
 constexpr int NAT_CPF = 8;      /* tiles per lane held in registers by k_native_carry */
 __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS) {
     const int f = blockIdx.x;
-    if (f >= A.n_files || !A.active[f]) return;
+    if (f >= A.n_files) return;
+    if (A.io.flags && threadIdx.x == 0) init_out_one(A.io, f);   /* k_init_out's work for f */
+    if (!A.active[f]) return;
     const int lane = threadIdx.x;
     const int64_t nd = A.doff[f + 1] - A.doff[f];
     const int64_t nb = nd - 1;
@@ -1832,7 +1835,8 @@ HbTables *hb_tables(bpmx_ctx *ctx, int64_t nd, int window, HilbPlan *P, size_t *
 
 int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, const bpmx_out *O, hipStream_t s,
                     int F, const std::vector<int64_t> &foff, const std::vector<int64_t> &doff, int64_t maxnd,
-                    const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active, const QuantArgs *qa) {
+                    const int64_t *d_foff, const int64_t *d_doff, const int32_t *d_active, const QuantArgs *qa,
+                    const InitOutArgs *io) {
     const int ds = P->ds;
     if (ds > NAT_DSMAX) return fail(BPMX_E_LIMIT, "native mode supports ds <= " + std::to_string(NAT_DSMAX));
     int rc = BPMX_OK;
@@ -1896,6 +1900,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     const double *d_tt = d_tab + TB_COEF + 8 * (size_t)(ds + 1);
     mfma_off = TB_COEF + 8 * (size_t)(ds + 1) + TT_SIZE;
     /* geometry: block offsets, per-file tile offsets, the tile list (cached with the context) */
+    const int64_t gstr = (bt + 15) / 16 * 16;                 /* gamma row per tile */
     std::vector<int64_t> tk(4 + 2 * (F + 1));
     tk[0] = bt; tk[1] = F; tk[2] = ds; tk[3] = 0;
     for (int f = 0; f <= F; ++f) { tk[4 + f] = foff[f]; tk[5 + F + f] = doff[f]; }
@@ -1908,8 +1913,11 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             geo[f + 1] = geo[f] + nb;
             geo[F + 1 + f] = (int64_t)tv.size();
             if (nd <= 15) continue;                          /* inactive (filtfilt would raise) */
+            /* gamma: one 128-byte aligned row of gstr doubles per tile, so
+             * k_native_blocks writes and k_native_yd reads whole cache lines */
             for (int64_t j0 = 0; j0 < nb; j0 += bt)
-                tv.push_back(NatTile{foff[f] + j0 * ds, geo[f] + j0, doff[f] + j0, (int32_t)j0, (int32_t)nb, f, 0});
+                tv.push_back(NatTile{foff[f] + j0 * ds, (int64_t)tv.size() * gstr, doff[f] + j0, (int32_t)j0,
+                                     (int32_t)nb, f, 0});
         }
         geo[2 * F + 1] = (int64_t)tv.size();
         ctx->nat_boff = geo;
@@ -1919,7 +1927,6 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         ctx->nat_tiles_dirty = true;
     }
     const int64_t nt = (int64_t)(ctx->nat_tiles.size() / sizeof(NatTile));
-    const int64_t sum_blocks = ctx->nat_boff[F];
     int64_t *d_geo = (int64_t *)ctx->buf("nat_geo", (size_t)(F + 1) * 16, &rc, &grew);
     if (grew) ctx->nat_tiles_dirty = true;
     NatTile *d_tiles = (NatTile *)ctx->buf("nat_tiles", std::max<size_t>(ctx->nat_tiles.size(), 64), &rc, &grew);
@@ -1931,7 +1938,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             HIP_TRY(hipMemcpyAsync(d_tiles, ctx->nat_tiles.data(), ctx->nat_tiles.size(), hipMemcpyHostToDevice, s));
         ctx->nat_tiles_dirty = false;
     }
-    double *gam = (double *)ctx->buf("nat_gam", (size_t)std::max<int64_t>(sum_blocks, 1) * 8, &rc);
+    double *gam = (double *)ctx->buf("nat_gam", (size_t)std::max<int64_t>(nt * gstr, 1) * 8, &rc);
     double *agg = (double *)ctx->buf("nat_agg", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
     double *carry = (double *)ctx->buf("nat_carry", (size_t)std::max<int64_t>(nt, 1) * 64, &rc);
     double *part = (double *)ctx->buf("nat_part", (size_t)F * 64 * NAT_PART * 8, &rc);
@@ -2013,6 +2020,8 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.pcm = B->pcm; a.foff = d_foff; a.doff = d_doff; a.boff = d_geo; a.toff = d_geo + F + 1;
         a.active = d_active; a.n_files = F; a.dtype = P->dtype; a.channels = P->channels; a.ds = ds; a.bt = bt;
         a.tab = d_tab; a.tt = d_tt; a.agg = agg; a.part = part; a.carry = carry; a.yd = yd;
+        if (io) a.io = *io;
+        else a.io = InitOutArgs{};
         SosStep ss;
         for (int i = 0; i < 12; ++i) ss.s[i] = P->sos[i];
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);

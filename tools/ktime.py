@@ -1,7 +1,7 @@
 """A/B kernel timing of library builds on the metric batch (no parity check:
 diagnostic builds may produce wrong outputs).
 
-    python tools/ktime.py [--steps K] [--files F] lib1.so lib2.so ...
+    python tools/ktime.py [--steps K] [--files F] lib1.so lib2.so[,VAR=VALUE...] ...
 
 Each build runs in its own child process (BPMX_LIB), alternating twice:
 step time (events around bpmx_run) and per-kernel device time from a fully
@@ -61,16 +61,18 @@ def main():
         else:
             libs.append(a)
     for rep in range(2):
-        for lib in libs:
+        for spec in libs:
+            lib, *kv = spec.split(",")
             env = dict(os.environ, BPMX_LIB=lib)
+            env.update(x.split("=", 1) for x in kv)
             r = subprocess.run([sys.executable, "-c", CHILD, str(files), str(steps), mode], env=env,
                                capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
-                print(lib, "FAILED", r.stderr[-2000:], flush=True)
+                print(spec, "FAILED", r.stderr[-2000:], flush=True)
                 sys.exit(1)
             d = json.loads(r.stdout.strip().splitlines()[-1])
             ks = {k: round(v, 4) for k, v in sorted(d["k"].items(), key=lambda kv: -kv[1]) if v > 0.02}
-            print(f"{lib} step {d['step_ms']:.4f} ms {ks}", flush=True)
+            print(f"{spec} step {d['step_ms']:.4f} ms {ks}", flush=True)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,7 @@ for s in "$@"; do
     stage) step stage 600 rocprofv3 --kernel-trace --marker-trace --hip-runtime-trace --output-format csv -d $O/prof_stage -o run -- python3 bench.py --steps 3 --warmup 1 $Q ;;
     fetch) step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch -o run -- python3 bench.py --steps 3 --warmup 1 $Q ;;
     write) step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 $Q ;;
+    kt) step ktime 900 python tools/ktime.py ${KT:-build_var/libbpmx_head.so bpm_analysis_amd/libbpmx.so} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown $s"; exit 2 ;;
   esac
