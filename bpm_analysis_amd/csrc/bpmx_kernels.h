@@ -372,7 +372,7 @@ struct DraftBoundArgs {
  * workgroup, one wave per trough */
 constexpr int DP_CHUNK = 32;
 constexpr int DB_T = 256;
-constexpr int DB_TRMAX = 2048;   /* troughs per recording staged in LDS */
+constexpr int DB_TRMAX = 2040;   /* troughs per recording staged in LDS (k_draft_bounds: four workgroups per CU) */
 constexpr int DB_LOCAL_M = 512;  /* more troughs than this: per-window ranking instead of the global order */
 struct DbSeg {                   /* a trough-curve segment [s, e) and one of its end values */
     int32_t s, e;
