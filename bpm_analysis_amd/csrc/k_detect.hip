@@ -877,24 +877,37 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         }
         const double thr = A.qv[(int64_t)f * Q_SLOTS + A.qslot];
         const double *bh2 = s_bh + FL_B1, *bh3 = s_bh + FL_B1 + FL_B2;
-        for (int j = tid; j < M; j += FP_T) {
-            const uint8_t sj = ld_state(&s_st[j]);
+        /* the kept maxima, compacted (in order) into the recording's stretch
+         * of the state scratch (2 bytes each; at most n / 2 of them), so the
+         * walks run on ~K / 64 full waves instead of every wave's few kept
+         * lanes; the distance filter's removals get the tie check first */
+        int16_t *kl = reinterpret_cast<int16_t *>(A.state + ((d0 + 1) & ~(int64_t)1));
+        int K = 0;
+        for (int q0 = 0; q0 < M; q0 += FP_T) {
+            const int j = q0 + tid;
+            const uint8_t sj = j < M ? s_st[j] : (uint8_t)ST_HEIGHT;
             if (sj == ST_REMOVED) {
                 /* removed by the distance filter: a decisive tie (include/bpmx.h
                  * BPMX_F_*_TIE) unless a strictly higher candidate the filter
-                 * kept lies within dist (its state may already carry the
-                 * prominence outcome: every kept state is odd) */
+                 * kept lies within dist */
                 const int64_t pj = s_mp[j];
                 const double vj = s_mh[j];
                 bool dom = false;
                 for (int k = j - 1; !dom && k >= 0 && pj - s_mp[k] < dist; --k)
-                    dom = s_mh[k] > vj && st_kept_by_distance(ld_state(&s_st[k]));
+                    dom = s_mh[k] > vj && st_kept_by_distance(s_st[k]);
                 for (int k = j + 1; !dom && k < M && s_mp[k] - pj < dist; ++k)
-                    dom = s_mh[k] > vj && st_kept_by_distance(ld_state(&s_st[k]));
+                    dom = s_mh[k] > vj && st_kept_by_distance(s_st[k]);
                 if (!dom) s_tie = 1;
-                continue;
             }
-            if (sj != ST_KEPT) continue;
+            int tot;
+            const int off = block_scan_flag<FP_T>(sj == ST_KEPT, sh, &tot);
+            if (sj == ST_KEPT) kl[K + off] = (int16_t)j;
+            K += tot;
+        }
+        __syncthreads();
+        STAMP(7);
+        for (int i = tid; i < K; i += FP_T) {
+            const int j = kl[i];
             const double hj = s_mh[j];
             double lmin = INF, rmin = INF;
             /* the two walks step together, and a step reads every candidate

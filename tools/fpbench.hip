@@ -49,9 +49,15 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&d_nout, F * 4));
     CK(hipMalloc(&d_state, env.size()));
     CK(hipMalloc(&d_st, (size_t)F * 16 * 8));
-    int32_t *d_vc, *d_fb;
+    int32_t *d_vc, *d_fb, *d_sok, *d_scnt;
+    double *d_cval, *d_vval, *d_outv;
     CK(hipMalloc(&d_vc, env.size() * 4));
     CK(hipMalloc(&d_fb, F * 4));
+    CK(hipMalloc(&d_sok, F * 4));
+    CK(hipMalloc(&d_scnt, (size_t)F * FPS_NW * 2 * 4));
+    CK(hipMalloc(&d_cval, env.size() * 8));
+    CK(hipMalloc(&d_vval, env.size() * 8));
+    CK(hipMalloc(&d_outv, env.size() * 8));
     CK(hipMemcpy(d_env, env.data(), env.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_qv, qv.data(), qv.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_doff, doff.data(), (F + 1) * 8, hipMemcpyHostToDevice));
@@ -67,6 +73,10 @@ int main(int argc, char **argv) {
         a.sign = sg; a.cand = d_cand; a.state = d_state; a.out = d_out; a.nout = d_nout; a.run_out = nullptr;
         a.run_min = 0; a.stamps = d_st; a.vcand = d_vc; a.fallback = d_fb; a.only = nullptr; a.lds_nmax = INT64_MAX;
         a.flags = nullptr; a.tie_bit = 0;
+        /* as in the pipeline: the trough launch scans and records, the peak
+         * launch takes its lists; values beside the trough indices */
+        a.cval = d_cval; a.vval = d_vval; a.scan_ok = d_sok; a.scan_cnt = d_scnt;
+        a.outv = sg < 0 ? d_outv : nullptr;
         const bool lds = argc > 2 && argv[2][0] == 'l';
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
@@ -75,6 +85,7 @@ int main(int argc, char **argv) {
         for (int rep = 0; rep < 5; ++rep) {
             CK(hipEventRecord(e0, 0));
             CK(hipMemset(d_st, 0, (size_t)F * 16 * 8));
+            if (sg < 0) CK(hipMemset(d_sok, 0, F * 4));
             if (lds) hipLaunchKernelGGL(k_find_peaks_lds, dim3(F), dim3(FP_T), 0, 0, a);
             else hipLaunchKernelGGL(k_find_peaks, dim3(F), dim3(FP_T), 0, 0, a);
             CK(hipEventRecord(e1, 0));
@@ -94,7 +105,7 @@ int main(int argc, char **argv) {
         long long np = 0;
         for (auto v : no) np += v;
         const char *names0[8] = {"tables", "maxima", "distance", "prominence", "compact", "(prom max wave)", "(prom mean wave)", "-"};
-        const char *names1[8] = {"-", "extrema", "to LDS", "dist:rounds", "prominence", "compact", "dist:lists", "-"};
+        const char *names1[8] = {"-", "extrema", "to LDS", "dist:rounds", "prom:walks", "compact", "dist:lists", "prom:prep"};
         const char **names = lds ? names1 : names0;
         printf("sign %+.0f: %.3f ms, %lld peaks; per-WG cycles %.0f\n", sg, best, np, tot / F);
         for (int k = 0; k < 8; ++k)
