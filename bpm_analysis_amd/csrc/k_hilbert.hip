@@ -539,54 +539,46 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
      * envelope's tolerance is 1e-9 relative), edge windows divide */
     const double invw = 1.0 / (double)w;
     auto mean = [&](double sum, int64_t cnt) { return cnt == w ? sum * invw : sum / (double)cnt; };
-    int64_t sa, ea, sz, ez;
-    win_bounds(i0, N, w, sa, ea);
-    win_bounds(i1 - 1, N, w, sz, ez);
-    if (i0 < i1 && ez - ea == i1 - 1 - i0 && sz - sa == i1 - 1 - i0) {
-        /* both window ends slide by one per output: the same operations in
-         * the same order, with every LDS read issued before the sums */
-        const int cnt = i1 - i0;
+    /* one code path for every run: each output adds the sample entering at the
+     * right (none once the window reaches N) and drops the one leaving at the
+     * left (none while the window starts at 0); an absent sample adds or
+     * drops 0.0, which leaves the sum bit for bit as the sliding sum had it.
+     * Every LDS read is issued before the sums.  (A run holding edge windows
+     * took a per-output bounds-and-loops path: the first and last threads
+     * were the phase's critical path, 18 K cycles against ~5 K.) */
+    if (i0 < i1) {
+        const int cnt = i1 - i0, offw = (int)((w - 1) / 2) + 1, wi = (int)w;
+        /* window of output i: [max(i + offw - w, 0), min(i + offw, N)) */
+        auto we = [&](int i) { return min(i + offw, N); };
+        auto ws = [&](int i) { return max(i + offw - wi, 0); };
         double ad[HB_RMPER], sb[HB_RMPER];
 #pragma unroll
-        for (int j = 1; j < HB_RMPER; ++j)
-            if (j < cnt) { ad[j] = mag[ea + j - 1]; sb[j] = mag[sa + j - 1]; }
+        for (int j = 1; j < HB_RMPER; ++j) {
+            const int i = i0 + j;
+            ad[j] = (j < cnt && we(i) > we(i - 1)) ? mag[we(i) - 1] : 0.0;
+            sb[j] = (j < cnt && ws(i) > ws(i - 1)) ? mag[ws(i - 1)] : 0.0;
+        }
         double sum = 0.0;
-        for (int64_t q = sa; q < ea; ++q) sum += mag[q];
-        const int64_t c = ea - sa;
-        ev[0] = mean(sum, c);
+        for (int q = ws(i0); q < we(i0); ++q) sum += mag[q];
+        ev[0] = mean(sum, we(i0) - ws(i0));
 #pragma unroll
         for (int j = 1; j < HB_RMPER; ++j)
             if (j < cnt) {
                 sum += ad[j];
                 sum -= sb[j];
-                ev[j] = mean(sum, c);
+                ev[j] = mean(sum, we(i0 + j) - ws(i0 + j));
             }
-    } else if (i0 < i1) {
-        int64_t s, e;
-        win_bounds(i0, N, w, s, e);
-        double sum = 0.0;
-        for (int64_t q = s; q < e; ++q) sum += mag[q];
-        ev[0] = mean(sum, e - s);
-#pragma unroll
-        for (int j = 1; j < HB_RMPER; ++j) {
-            const int i = i0 + j;
-            if (i < i1) {
-                int64_t s2, e2;
-                win_bounds(i, N, w, s2, e2);
-                for (int64_t q = e; q < e2; ++q) sum += mag[q];
-                for (int64_t q = s; q < s2; ++q) sum -= mag[q];
-                s = s2; e = e2;
-                ev[j] = mean(sum, e - s);
-            }
-        }
     }
+    STAMP(8);
     /* through LDS, so the global stores are coalesced */
     __syncthreads();
+    STAMP(9);
     double *stage = (double *)S.x;
 #pragma unroll
     for (int j = 0; j < HB_RMPER; ++j)
         if (i0 + j < i1) stage[i0 + j] = ev[j];
     __syncthreads();
+    STAMP(10);
     for (int i = threadIdx.x; i < N; i += HB_T) env[i] = stage[i];
     if (A.q.n_levels > 0 && N <= QR_MAX) {
         /* the detection stage's quantiles from the staged envelope (the same
@@ -673,6 +665,11 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
     P->nrtab = any_rd ? 2 * (HB_RD_P - 1) : 0;
     P->per = (int32_t)((nd + HB_T - 1) / HB_T);
     if (P->per > HB_RMPER) return 0;
+#ifdef HB_ODDPER
+    /* an odd run length: the threads' runs start an odd number of doubles
+     * apart, so a wave's LDS reads along the runs conflict at most 2-way */
+    if ((P->per & 1) == 0 && P->per + 1 <= HB_RMPER) P->per += 1;
+#endif
     *lds_bytes = (size_t)(M + P->ntwh + 128 + np + P->nrtab) * sizeof(double2);
     if (*lds_bytes > HB_LDS_MAX) return 0;
     tabs->resize((size_t)P->ntwh + 128 + np + P->nrtab);

@@ -51,13 +51,13 @@ static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> 
     CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
     env_out.resize(y.size());
     CK(hipMemcpy(env_out.data(), denv, y.size() * 8, hipMemcpyDeviceToHost));
-    double acc[8] = {0};
-    for (int f = 0; f < F; ++f) for (int k = 0; k < 8; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
+    double acc[11] = {0};
+    for (int f = 0; f < F; ++f) for (int k = 0; k < 11; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
     printf("kernel %.4f ms;  mean cycles per workgroup (s_memtime):", ms / R);
-    const char *nm[8] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "rollmean"};
+    const char *nm[11] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "store", "rollsum", "rm:barrier", "stage"};
     double tot = 0;
-    for (int k = 0; k < 8; ++k) tot += acc[k] / F;
-    for (int k = 0; k < 8; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
+    for (int k = 0; k < 11; ++k) tot += acc[k] / F;
+    for (int k = 0; k < 11; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
     printf("\n");
     CK(hipFree(dy)); CK(hipFree(denv)); CK(hipFree(dd)); CK(hipFree(da)); CK(hipFree(dt)); CK(hipFree(dst));
     return ms / R;
