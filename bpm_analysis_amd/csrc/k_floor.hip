@@ -686,8 +686,10 @@ constexpr int DP_FIX = 4;         /* exact steps after a segment's inverse estim
 template <int DP_SPL>
 __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s_tv, int base, int m, int64_t n,
                                             int64_t lo, int64_t hi, int jl, int jh, double q, uint32_t seed,
-                                            double *res, double seedv = __builtin_nan(""), double *rho = nullptr) {
+                                            double *res, double seedv = __builtin_nan(""), double *rho = nullptr,
+                                            double theta = __builtin_nan(""), int *decided = nullptr) {
     const int lane = lane_id();
+    if (decided) *decided = -1;
     if (jh - jl + 1 > 64 * DP_SPL) return false;
     int32_t sa[DP_SPL], sn[DP_SPL], st[DP_SPL], slo[DP_SPL], shi[DP_SPL], sub[DP_SPL];
     double sy[DP_SPL], ssl[DP_SPL], sinv[DP_SPL];
@@ -735,7 +737,18 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
     uint32_t rng = seed;
     bool seed_down = false;
     int64_t seed_nless = 0, seed_nleq = 0;
+    /* decision mode (theta = env[t] / mult, finite): the caller needs only
+     * whether env[t] <= mult * value.  The first two pivots are theta pushed
+     * up and down by 2^-48 (far beyond the rounding of the division and of
+     * mult * value): fewer than k + 1 elements below the upper one puts s_k,
+     * hence the value, above it (keep); at least k + 2 (k + 1 without
+     * interpolation) below the lower one puts s_(k+1) (s_k), hence the value,
+     * under it (drop).  Either ends the selection after one or two counts;
+     * otherwise the rounds go on from the narrowed active set. */
+    const bool dmode = decided && __builtin_isfinite(theta);
+    const int ib = dmode ? 2 : 0;
     for (int it = 0; it < 256; ++it) {
+        const int it2 = it - ib;
         int cnt = 0;
 #pragma unroll
         for (int r = 0; r < DP_SPL; ++r) cnt += shi[r] - slo[r];
@@ -794,16 +807,18 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             return true;
         }
         double pv;
-        if (it == 0 && __builtin_isfinite(seedv)) {
+        if (it < ib) {
+            pv = it == 0 ? theta * (1.0 + 0x1p-48) : theta * (1.0 - 0x1p-48);
+        } else if (it2 == 0 && __builtin_isfinite(seedv)) {
             /* the neighbouring trough's draft value: its window overlaps this
              * one but for a few segments, so the count there lands near k */
             pv = seedv;
-        } else if (it == 1 && __builtin_isfinite(seedv) && rho && *rho > 0.0 && __builtin_isfinite(*rho)) {
+        } else if (it2 == 1 && __builtin_isfinite(seedv) && rho && *rho > 0.0 && __builtin_isfinite(*rho)) {
             /* then a step from it by the count still missing over the
              * neighbour's density of values near its answer */
             pv = seed_down ? seedv - ((double)(seed_nless - k) - 0.5) / *rho
                            : seedv + ((double)(k - seed_nleq) + 0.5) / *rho;
-        } else if (it < DP_IP_ROUNDS) {
+        } else if (it2 < DP_IP_ROUNDS) {
             /* a value pivot interpolated between the active extremes at the
              * target's rank: the values within a segment are evenly spaced, so
              * the active set shrinks by far more than a random pivot's half */
@@ -886,7 +901,9 @@ __device__ __forceinline__ bool draft_point(const int32_t *s_tp, const double *s
             ce += sub[r] - slo[r];
         }
         const int64_t nless = below + wave_sum_i(cl), nleq = below + wave_sum_i(ce);
-        if (it == 0) { seed_down = k < nless; seed_nless = nless; seed_nleq = nleq; }
+        if (it == 0 && dmode && nless <= k) { *decided = 1; return true; }
+        if (it == 1 && dmode && nless >= k + (interp ? 2 : 1)) { *decided = 0; return true; }
+        if (it2 == 0) { seed_down = k < nless; seed_nless = nless; seed_nleq = nleq; }
         if (k < nless) {
 #pragma unroll
             for (int r = 0; r < DP_SPL; ++r) shi[r] = slb[r];
@@ -1227,12 +1244,22 @@ __device__ __forceinline__ void draft_points_chunk(const DraftBoundArgs &A, int 
             continue;
         }
         const uint32_t seed = 0x9E3779B9u * (uint32_t)(f + 1) ^ (uint32_t)j * 0x85EBCA6Bu;
-        if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r, prev, &rho)) {
+        /* only the keep decision is needed: draft_point's decision mode
+         * settles most troughs with one or two counts against env / mult */
+        const double et = s_tv[j - base];
+        const double theta = A.mult > 0.0 ? et / A.mult : __builtin_nan("");
+        int dd = -1;
+        if (!draft_point<SPL>(s_tp, s_tv, base, m, n, lo, hi, jl, jh, A.q, seed, &r, prev, &rho, theta, &dd)) {
             fail = true;
             continue;
         }
+        if (dd >= 0) {                                       /* decided without the value: no seed for the next */
+            prev = __builtin_nan("");
+            if (lane_id() == 0) A.dec[d0 + j] = (uint8_t)dd;
+            continue;
+        }
         prev = r;
-        if (lane_id() == 0) A.dec[d0 + j] = (r == r && s_tv[j - base] <= A.mult * r) ? 1 : 0;
+        if (lane_id() == 0) A.dec[d0 + j] = (r == r && et <= A.mult * r) ? 1 : 0;
     }
     if (fail && lane_id() == 0) __hip_atomic_store(&A.exact[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (A.stats && SPL == 1 && tid == 0) atomicAdd((unsigned long long *)&A.stats[1], (unsigned long long)nu);
