@@ -1219,7 +1219,11 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     }
     /* partial tile forward, tail, partial tile backward */
     V4 q{0, 0, 0, 0};
+#ifdef NAT_DIAG_NOTAIL
+    if (false) {                                            /* diagnostic: the serial tail's share (wrong yd) */
+#else
     if (lane == 0) {
+#endif
         double *pp = s_part;
         for (int b = 0; b < Lp; ++b) {
             double *r = pp + b * NAT_PART;
