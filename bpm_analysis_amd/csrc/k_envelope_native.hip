@@ -1235,6 +1235,10 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         const double xl = xt(n - 1);
         {
             V4 z = mv(Vm, S);                               /* the exact recursion runs in the original basis */
+#ifdef NAT_DIAG_NOSOS
+            for (int64_t k = 0; k < nt; ++k) s_ytl[k] = 0.0; /* diagnostic: the tail recursion's share (wrong yd) */
+            if (false)
+#endif
             for (int64_t k = 0; k < nt; ++k) {
                 const int64_t xi = base + k;
                 const double u = xi < n ? xt(xi) : odd_ext(wdt, xl, xt(n - 2 - (xi - n)));
@@ -1243,7 +1247,9 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         }
         const double y0 = s_ytl[nt - 1];
         q = V4{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
+#ifndef NAT_DIAG_NOSOS
         for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, s_ytl[k]);
+#endif
         q = mv(Vi, q);
         yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
         for (int b = Lp - 1; b >= 0; --b) {
