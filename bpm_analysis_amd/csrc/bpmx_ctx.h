@@ -48,6 +48,9 @@ struct bpmx_ctx {
     std::vector<char> nat_tiles;                /* host copy of the tile list */
     bool nat_tiles_dirty = false;
     bool nat_tab_dirty = false;
+    std::vector<double> nat_ttab;               /* tail tables of k_native_carry (host copy) */
+    std::vector<double> nat_tkey2;              /* their key: the sos coefficients and zi */
+    bool nat_ttab_dirty = false;
     bool prof = false;
     hipEvent_t stats_ev = nullptr;               /* recorded after the last run with BPMX_OPT_STATS */
     struct Rec { std::string name; hipEvent_t a, b; };

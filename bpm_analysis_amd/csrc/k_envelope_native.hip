@@ -103,7 +103,14 @@ struct NatCarryArgs {
     double *carry;                 /* [n_tiles][8]: S0_t, Qe_t */
     double *yd;
     InitOutArgs io;                /* io.flags non-null: reset recording f's outputs first */
+    const double *ttab;            /* tail tables (NAT_TT_ROWS rows of 16): C A^m | A^m B | A^m zi | h_m */
 };
+/* k_native_carry's tail recursion, lane-parallel: the exact per-sample
+ * recursion z' = A z + B u, y = C z + D u (SosStep, original basis) over the
+ * nt <= NAT_TT_PAR tail samples as its impulse response, row m of the tail
+ * table holding C A^m, A^m B, A^m zi and h_m (h_0 = D, h_m = C A^(m-1) B),
+ * built on the host in long double from the same coefficients */
+constexpr int NAT_TT_ROWS = NAT_DSMAX + 20, NAT_TT_PAR = 320;
 
 struct NatYdArgs {
     const NatTile *tiles;
@@ -1219,37 +1226,66 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     }
     /* partial tile forward, tail, partial tile backward */
     V4 q{0, 0, 0, 0};
-#ifdef NAT_DIAG_NOTAIL
-    if (false) {                                            /* diagnostic: the serial tail's share (wrong yd) */
-#else
     if (lane == 0) {
-#endif
         double *pp = s_part;
         for (int b = 0; b < Lp; ++b) {
             double *r = pp + b * NAT_PART;
             r[12] = S.a; r[13] = S.b; r[14] = S.c; r[15] = S.d;
             S = add4(mv(Mm, S), V4{r[0], r[1], r[2], r[3]});
         }
-        auto xt = [&](int64_t k) { return s_tail[k - tlo]; };   /* k in [tlo, n) */
-        const int64_t nt = ntl + 15;                            /* tail length incl. right pad */
-        const double xl = xt(n - 1);
-        {
-            V4 z = mv(Vm, S);                               /* the exact recursion runs in the original basis */
-#ifdef NAT_DIAG_NOSOS
-            for (int64_t k = 0; k < nt; ++k) s_ytl[k] = 0.0; /* diagnostic: the tail recursion's share (wrong yd) */
-            if (false)
-#endif
-            for (int64_t k = 0; k < nt; ++k) {
-                const int64_t xi = base + k;
-                const double u = xi < n ? xt(xi) : odd_ext(wdt, xl, xt(n - 2 - (xi - n)));
-                s_ytl[k] = SS.step(z, u);
-            }
+    }
+    S = V4{__shfl(S.a, 0), __shfl(S.b, 0), __shfl(S.c, 0), __shfl(S.d, 0)};
+    auto xt = [&](int64_t k) { return s_tail[k - tlo]; };   /* k in [tlo, n) */
+    const int64_t nt = ntl + 15;                            /* tail length incl. right pad */
+    const double xl = xt(n - 1);
+    auto tin = [&](int64_t k) {                             /* tail input k: the samples, then the odd extension */
+        const int64_t xi = base + k;
+        return xi < n ? xt(xi) : odd_ext(wdt, xl, xt(n - 2 - (xi - n)));
+    };
+    if (A.ttab && nt <= NAT_TT_PAR) {
+        /* lane-parallel: y_k = C A^k z0 + sum_(m <= k) h_m u_(k-m), then the
+         * backward pass's final state q = A^(nt-1) zi y_(nt-1) +
+         * sum_(k >= 1) A^(k-1) B y_k as a wave sum (agrees with the serial
+         * recursion to rounding; that took half of this kernel on lane 0) */
+        const V4 z0 = mv(Vm, S);
+        for (int64_t k = lane; k < nt; k += 64) {
+            const double *tr = A.ttab + k * 16;
+            double y = dot4(V4{tr[0], tr[1], tr[2], tr[3]}, z0);
+            for (int64_t m = 0; m <= k; ++m) y = __builtin_fma(A.ttab[m * 16 + 12], tin(k - m), y);
+            s_ytl[k] = y;
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double y0 = s_ytl[nt - 1];
+        V4 acc{0, 0, 0, 0};
+        for (int64_t k = 1 + lane; k < nt; k += 64) {
+            const double *tr = A.ttab + (k - 1) * 16 + 4;
+            const double yk = s_ytl[k];
+            acc = V4{__builtin_fma(tr[0], yk, acc.a), __builtin_fma(tr[1], yk, acc.b), __builtin_fma(tr[2], yk, acc.c),
+                     __builtin_fma(tr[3], yk, acc.d)};
+        }
+        for (int o = 32; o > 0; o >>= 1)
+            acc = V4{acc.a + __shfl_xor(acc.a, o), acc.b + __shfl_xor(acc.b, o), acc.c + __shfl_xor(acc.c, o),
+                     acc.d + __shfl_xor(acc.d, o)};
+        const double *tz = A.ttab + (nt - 1) * 16 + 8;
+        q = V4{__builtin_fma(tz[0], y0, acc.a), __builtin_fma(tz[1], y0, acc.b), __builtin_fma(tz[2], y0, acc.c),
+               __builtin_fma(tz[3], y0, acc.d)};
+    } else if (lane == 0) {
+        V4 z = mv(Vm, S);                                   /* the exact recursion runs in the original basis */
+#ifdef NAT_DIAG_NOSOS
+        for (int64_t k = 0; k < nt; ++k) s_ytl[k] = 0.0;    /* diagnostic: the tail recursion's share (wrong yd) */
+        if (false)
+#endif
+        for (int64_t k = 0; k < nt; ++k) s_ytl[k] = SS.step(z, tin(k));
         const double y0 = s_ytl[nt - 1];
         q = V4{zi.a * y0, zi.b * y0, zi.c * y0, zi.d * y0};
 #ifndef NAT_DIAG_NOSOS
         for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, s_ytl[k]);
 #endif
+    }
+    if (lane == 0) {
+        double *pp = s_part;
         q = mv(Vi, q);
         yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
         for (int b = Lp - 1; b >= 0; --b) {
@@ -2034,6 +2070,67 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         else a.io = InitOutArgs{};
         SosStep ss;
         for (int i = 0; i < 12; ++i) ss.s[i] = P->sos[i];
+        /* the tail tables (rebuilt when the coefficients change): row m holds
+         * C A^m, A^m B, A^m zi and h_m of SosStep's recursion, in long double */
+        std::vector<double> key2(P->sos, P->sos + 12);
+        key2.insert(key2.end(), ctx->nat_tab.begin() + TB_ZI, ctx->nat_tab.begin() + TB_ZI + 4);
+        if (key2 != ctx->nat_tkey2) {
+            typedef long double LD;
+            LD c[12];
+            for (int i = 0; i < 12; ++i) c[i] = (LD)P->sos[i];
+            auto step = [&](LD z[4], LD u) -> LD {                /* SosStep::step */
+                const LD x1 = c[0] * u + z[0];
+                const LD z00 = c[1] * u - c[4] * x1 + z[1];
+                const LD z01 = c[2] * u - c[5] * x1;
+                const LD y = c[6] * x1 + z[2];
+                const LD z10 = c[7] * x1 - c[10] * y + z[3];
+                const LD z11 = c[8] * x1 - c[11] * y;
+                z[0] = z00; z[1] = z01; z[2] = z10; z[3] = z11;
+                return y;
+            };
+            LD Am[4][4], Bv[4], Cv[4], Dv;
+            for (int i = 0; i < 4; ++i) {
+                LD z[4] = {0, 0, 0, 0};
+                z[i] = 1;
+                Cv[i] = step(z, 0);
+                for (int r = 0; r < 4; ++r) Am[r][i] = z[r];
+            }
+            {
+                LD z[4] = {0, 0, 0, 0};
+                Dv = step(z, 1);
+                for (int r = 0; r < 4; ++r) Bv[r] = z[r];
+            }
+            LD ca[4], g[4], az[4];
+            for (int i = 0; i < 4; ++i) { ca[i] = Cv[i]; g[i] = Bv[i]; az[i] = (LD)ctx->nat_tab[TB_ZI + i]; }
+            std::vector<double> &tt2 = ctx->nat_ttab;
+            tt2.assign((size_t)NAT_TT_ROWS * 16, 0.0);
+            LD hprev = Dv;
+            for (int m = 0; m < NAT_TT_ROWS; ++m) {
+                double *row = tt2.data() + (size_t)m * 16;
+                for (int i = 0; i < 4; ++i) { row[i] = (double)ca[i]; row[4 + i] = (double)g[i]; row[8 + i] = (double)az[i]; }
+                row[12] = (double)hprev;                     /* h_m: D, then C A^(m-1) B */
+                LD hn = 0;
+                for (int i = 0; i < 4; ++i) hn += ca[i] * Bv[i];
+                hprev = hn;
+                LD ca2[4], g2[4], az2[4];
+                for (int j = 0; j < 4; ++j) {
+                    ca2[j] = 0; g2[j] = 0; az2[j] = 0;
+                    for (int i = 0; i < 4; ++i) { ca2[j] += ca[i] * Am[i][j]; g2[j] += Am[j][i] * g[i]; az2[j] += Am[j][i] * az[i]; }
+                }
+                for (int j = 0; j < 4; ++j) { ca[j] = ca2[j]; g[j] = g2[j]; az[j] = az2[j]; }
+            }
+            ctx->nat_tkey2 = key2;
+            ctx->nat_ttab_dirty = true;
+        }
+        bool grew2 = false;
+        double *d_tt2 = (double *)ctx->buf("nat_ttab", (size_t)NAT_TT_ROWS * 16 * 8, &rc, &grew2);
+        if (rc != BPMX_OK) return rc;
+        if (grew2) ctx->nat_ttab_dirty = true;
+        if (ctx->nat_ttab_dirty) {
+            HIP_TRY(hipMemcpyAsync(d_tt2, ctx->nat_ttab.data(), ctx->nat_ttab.size() * 8, hipMemcpyHostToDevice, s));
+            ctx->nat_ttab_dirty = false;
+        }
+        a.ttab = std::getenv("BPMX_CARRY_SERIAL") ? nullptr : d_tt2;   /* (A/B: the serial tail) */
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
     }
     if (nt > 0) {
