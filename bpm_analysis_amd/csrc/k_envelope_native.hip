@@ -1226,15 +1226,38 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
     }
     /* partial tile forward, tail, partial tile backward */
     V4 q{0, 0, 0, 0};
-    if (lane == 0) {
-        double *pp = s_part;
-        for (int b = 0; b < Lp; ++b) {
-            double *r = pp + b * NAT_PART;
-            r[12] = S.a; r[13] = S.b; r[14] = S.c; r[15] = S.d;
-            S = add4(mv(Mm, S), V4{r[0], r[1], r[2], r[3]});
+    /* the partial tile's block recursions, S_(b+1) = M S_b + u_b forward and
+     * q_b = M q_(b+1) + P S_b + v_b backward, as lane scans (lane b = block b,
+     * Lp <= 63; M in modal coordinates is two rotation blocks) */
+    const Cx2 M1{Mm.m[0], Mm.m[1], Mm.m[10], Mm.m[11]};
+    double *pp = s_part;
+    {
+        Cx2 P = lane < Lp ? M1 : ID;
+        V4 acc = lane < Lp ? V4{pp[lane * NAT_PART + 0], pp[lane * NAT_PART + 1], pp[lane * NAT_PART + 2],
+                                pp[lane * NAT_PART + 3]}
+                           : Z4;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int d = 1 << k;
+            const Cx2 Pe = shfl_up_cx2(P, d);
+            const V4 ae = shfl_up_v(acc, d);
+            if (lane >= d) {
+                acc = add4(cx2_mv(P, ae), acc);
+                P = cx2_mul(P, Pe);
+            }
         }
+        const V4 Sn = add4(cx2_mv(P, S), acc);                  /* S_(b+1) */
+        V4 Sb = shfl_up_v(Sn, 1);
+        if (lane == 0) Sb = S;
+        if (lane < Lp) {
+            double *r = pp + lane * NAT_PART;
+            r[12] = Sb.a; r[13] = Sb.b; r[14] = Sb.c; r[15] = Sb.d;
+        }
+        if (Lp > 0) S = V4{__shfl(Sn.a, Lp - 1), __shfl(Sn.b, Lp - 1), __shfl(Sn.c, Lp - 1), __shfl(Sn.d, Lp - 1)};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    S = V4{__shfl(S.a, 0), __shfl(S.b, 0), __shfl(S.c, 0), __shfl(S.d, 0)};
     auto xt = [&](int64_t k) { return s_tail[k - tlo]; };   /* k in [tlo, n) */
     const int64_t nt = ntl + 15;                            /* tail length incl. right pad */
     const double xl = xt(n - 1);
@@ -1284,18 +1307,34 @@ __global__ __launch_bounds__(64) void k_native_carry(NatCarryArgs A, SosStep SS)
         for (int64_t k = nt - 1; k >= 1; --k) (void)SS.step(q, s_ytl[k]);
 #endif
     }
-    if (lane == 0) {
-        double *pp = s_part;
-        q = mv(Vi, q);
-        yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
-        for (int b = Lp - 1; b >= 0; --b) {
-            const double *r = pp + b * NAT_PART;
-            const V4 Sj{r[12], r[13], r[14], r[15]};
-            q = add4(mv(Mm, q), add4(mv(Pm, Sj), V4{r[4], r[5], r[6], r[7]}));
-            yd[Tf * bt + b] = dot4(Cv, q) + Dd * (dot4(Cv, Sj) + Dd * r[8]);
-        }
-    }
     q = V4{__shfl(q.a, 0), __shfl(q.b, 0), __shfl(q.c, 0), __shfl(q.d, 0)};
+    q = mv(Vi, q);
+    if (lane == 0) yd[nd - 1] = dot4(Cv, q) + Dd * s_ytl[0];
+    {
+        V4 Sj{0, 0, 0, 0}, w{0, 0, 0, 0};
+        double xj = 0.0;
+        if (lane < Lp) {
+            const double *r = pp + lane * NAT_PART;
+            Sj = V4{r[12], r[13], r[14], r[15]};
+            w = add4(mv(Pm, Sj), V4{r[4], r[5], r[6], r[7]});
+            xj = r[8];
+        }
+        Cx2 P = lane < Lp ? M1 : ID;
+        V4 acc = w;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int d = 1 << k;
+            const Cx2 Pe = shfl_down_cx2(P, d);
+            const V4 ae = shfl_down_v(acc, d);
+            if (lane + d < 64) {
+                acc = add4(cx2_mv(P, ae), acc);
+                P = cx2_mul(P, Pe);
+            }
+        }
+        const V4 qb = add4(cx2_mv(P, q), acc);                  /* q_b */
+        if (lane < Lp) yd[Tf * bt + lane] = dot4(Cv, qb) + Dd * (dot4(Cv, Sj) + Dd * xj);
+        q = V4{__shfl(qb.a, 0), __shfl(qb.b, 0), __shfl(qb.c, 0), __shfl(qb.d, 0)};
+    }
     /* backward tile carries: car[t][4..7] = Qe_t; Qe_(t-1) = M^T Qe_t + b_t.
      * Lane l's run maps the Qe entering its last tile to the Qe leaving its
      * first: (P, a) composed right to left; the scan runs from lane 63 down. */
