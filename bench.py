@@ -265,16 +265,44 @@ def oracle_outputs(mode: str, fs: int, n_frames: int, seeds, params: dict, threa
     return outs, time.perf_counter() - t0
 
 
-def compare_outputs(gpu: list, cpu: list, exact_env: bool) -> dict:
+TIE_BITS = 32 | 64                      # BPMX_F_TROUGH_TIE | BPMX_F_PEAK_TIE: decisive tie left open
+ORDERED_BITS = 128 | 256                # BPMX_F_*_ORDERED: re-decided in numpy's argsort order
+
+
+def numpy_order_expected(o: dict, fs: int, params: dict) -> dict:
+    """The oracle's troughs, floor, flags and peaks for the oracle envelope
+    o["env"] with find_peaks' distance filter in numpy's own argsort order
+    (what a tie-resolved GPU recording must equal, bpm_analysis.py:1070 / :227)."""
+    from oracle import oracle as O
+    d = O.derive(fs, params)
+    e = np.ascontiguousarray(o["env"])
+    fl, tr, flags, _ = O.noise_floor_numpy_order(e, d, params)
+    pk = O.find_peaks_numpy_order(e, height=fl, distance=d.distance,
+                                  prominence=O.quantile(e, params["peak_prominence_quantile"]))
+    return dict(o, floor=fl, troughs=tr, peaks=pk, flags=int(flags))
+
+
+def compare_outputs(gpu: list, cpu: list, exact_env: bool, fs: int = 0, params: dict | None = None) -> dict:
     """Per-file parity of the GPU batch against the oracle: every trough and
     peak index and the fallback flags bit-exact; env and floor bit-exact in
     reference mode, within 1e-9 x max|env| in native mode (north_star asks for
-    1e-5 relative).  Returns counts over files and the worst relative errors."""
+    1e-5 relative).  A GPU recording re-decided in numpy's order (an ORDERED
+    flag bit) is compared with the numpy-order oracle instead (needs `fs` and
+    `params`); one still carrying a decisive-tie bit counts in
+    `ties_unresolved`, and `ok` requires none.  Returns counts over files and
+    the worst relative errors."""
     n = len(cpu)
     pe = te = fe = 0
     env_rel = floor_rel = 0.0
     bad = []
+    unresolved = resolved = 0
     for f, (g, o) in enumerate(zip(gpu, cpu)):
+        gfl = int(g["flags"])
+        unresolved += bool(gfl & TIE_BITS)
+        if gfl & ORDERED_BITS:
+            resolved += 1
+            if params is not None:
+                o = numpy_order_expected(o, fs, params)
         scale = float(np.max(np.abs(o["env"]))) or 1.0
         de = float(np.max(np.abs(g["env"] - o["env"]))) / scale
         df = np.abs(g["floor"] - o["floor"])
@@ -284,7 +312,8 @@ def compare_outputs(gpu: list, cpu: list, exact_env: bool) -> dict:
         env_rel, floor_rel = max(env_rel, de), max(floor_rel, df)
         p_ok = np.array_equal(g["peaks"], o["peaks"])
         t_ok = np.array_equal(g["troughs"], o["troughs"])
-        f_ok = (int(g["flags"]) & FLOOR_FLAGS) == (int(o["flags"]) & FLOOR_FLAGS)
+        fmask = FLOOR_FLAGS & ~TIE_BITS if gfl & ORDERED_BITS else FLOOR_FLAGS
+        f_ok = (gfl & fmask) == (int(o["flags"]) & fmask)
         pe += p_ok
         te += t_ok
         fe += f_ok
@@ -293,7 +322,8 @@ def compare_outputs(gpu: list, cpu: list, exact_env: bool) -> dict:
     tol = 0.0 if exact_env else 1e-9
     return {"files": n, "peaks_equal": pe, "troughs_equal": te, "flags_equal": fe,
             "env_max_rel": env_rel, "floor_max_rel": floor_rel, "env_tol": tol,
-            "ok": pe == n and te == n and fe == n and env_rel <= tol and floor_rel <= tol,
+            "ties_resolved": resolved, "ties_unresolved": unresolved,
+            "ok": pe == n and te == n and fe == n and env_rel <= tol and floor_rel <= tol and unresolved == 0,
             "mismatched_files": bad}
 
 
@@ -302,7 +332,7 @@ def cpu_baseline(mode: str, fs: int, n_frames: int, seed0: int, n_files: int, pa
     timed, and the GPU outputs compared against it file by file."""
     threads, aff, ncpu = cpu_threads()
     outs, dt = oracle_outputs(mode, fs, n_frames, [seed0 + f for f in range(n_files)], params, threads)
-    parity = compare_outputs(gpu_host[:n_files], outs, exact_env=(mode == "reference"))
+    parity = compare_outputs(gpu_host[:n_files], outs, exact_env=(mode == "reference"), fs=fs, params=params)
     base = {"value": n_files * n_frames / dt, "unit": "audio-samples/s", "cores": threads, "kind": "port",
             "affinity_cpus": aff, "os_cpu_count": ncpu,
             "sample": f"the GPU batch's own {n_files} recordings (seeds {seed0}..{seed0 + n_files - 1}, "
@@ -405,6 +435,7 @@ def run_c5(args):
     npar = len(mine) if args.c5_parity_files < 0 else args.c5_parity_files
     pick = set(sorted(mine, key=lambda i: lengths[i])[:npar]) if not args.no_cpu else set()
     kept, rows, kprof = {}, [], {}
+    ties_c5 = [0]                       # recordings the steps' tie checks re-decided
     frames = nd_tot = 0
     elapsed = 0.0
     for ci in range(n_rounds):
@@ -429,12 +460,22 @@ def run_c5(args):
                 dets[k].run(pcm, fo, fs, params, mode="native", channels=ch, out=out, d=d, options=args.options)
 
             def step():
+                # every sub-batch's run, then its decisive-tie check (engine.resolve_ties)
+                checks = []
                 for sub in subs:
                     if streams[sub[0]] is None:
                         run_sub(sub)
+                        checks.append((sub, dets[sub[0]].tie_check_start(sub[4]), None))
                     else:
                         with torch.cuda.stream(streams[sub[0]]):
                             run_sub(sub)
+                            checks.append((sub, dets[sub[0]].tie_check_start(sub[4]), streams[sub[0]]))
+                for sub, h, st in checks:
+                    if st is None:
+                        ties_c5[0] += dets[sub[0]].tie_check_finish(h, sub[4], params, 7, args.options)
+                    else:
+                        with torch.cuda.stream(st):
+                            ties_c5[0] += dets[sub[0]].tie_check_finish(h, sub[4], params, 7, args.options)
 
             # per-kernel profile: the sub-batches one after another (untimed)
             for sub in subs:
@@ -486,16 +527,19 @@ def run_c5(args):
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(max(1, min(len(order), cpu_threads()[0]))) as ex:
             outs = list(ex.map(one, order))
-        parity = compare_outputs([kept[i] for i in order], outs, exact_env=False)
+        parity = compare_outputs([kept[i] for i in order], outs, exact_env=False, fs=fs, params=params)
         parity["files_checked_rank0"] = order
+        parity["tie_flagged_in_steps"] = ties_c5[0]
         if world > 1:
             cnt = torch.tensor([parity["files"], parity["peaks_equal"], parity["troughs_equal"],
-                                parity["flags_equal"], 0 if parity["ok"] else 1], dtype=torch.float64,
+                                parity["flags_equal"], 0 if parity["ok"] else 1, parity["ties_unresolved"],
+                                parity["ties_resolved"], ties_c5[0]], dtype=torch.float64,
                                device=det.device if backend == "nccl" else None)
             dist.all_reduce(cnt)
             c = [int(x) for x in cnt.tolist()]
             parity.update(files=c[0], peaks_equal=c[1], troughs_equal=c[2], flags_equal=c[3],
-                          ok=c[4] == 0, ranks=world)
+                          ok=c[4] == 0, ranks=world, ties_unresolved=c[5], ties_resolved=c[6],
+                          tie_flagged_in_steps=c[7])
     allres = gather_file_results(rows, len(lengths), device=det.device if (world > 1 and backend == "nccl") else None)
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -603,14 +647,37 @@ def main(args):
     out = det.alloc(fo, d.ds, d.sr)
     nd = -(-n // d.ds)
 
-    def step():
-        det.run(pcm, fo, fs, params, mode=args.mode, out=out, d=d, options=args.options)
+    def step(o=None):
+        det.run(pcm, fo, fs, params, mode=args.mode, out=out if o is None else o, d=d, options=args.options)
+
+    # The timed step is the drop-in's whole contract: the run, then the
+    # decisive-tie check (engine.resolve_ties: recordings whose find_peaks
+    # distance filter met equal heights are re-decided in numpy's argsort
+    # order, bpm_analysis.py:1070 / :227).  Two result sets alternate, so the
+    # check of step k (a flags read-back; a launch only when a bit is set)
+    # waits for step k while step k + 1 is already queued.
+    from bpm_analysis_amd import _native as N
+    outs_pp = [out, det.alloc(fo, d.ds, d.sr)]
+    ties = {"raised": 0, "resolved": 0}
+
+    def run_steps(k_steps):
+        pend = None
+        for k in range(k_steps):
+            o = outs_pp[k & 1]
+            step(o)
+            h = det.tie_check_start(o)
+            if pend is not None:
+                r = det.tie_check_finish(pend[0], pend[1], params, N.STAGE_ALL, args.options)
+                ties["raised"] += r
+            pend = (h, o)
+        if pend is not None:
+            ties["raised"] += det.tie_check_finish(pend[0], pend[1], params, N.STAGE_ALL, args.options)
+        return outs_pp[(k_steps - 1) & 1] if k_steps > 0 else out
 
     abytes = algorithmic_bytes(args.mode, F, n, nd, d.ds)
     # warmup with every launch bracketed by events: picks the dominant kernel
     det.profile(True)
-    for _ in range(args.warmup):
-        step()
+    run_steps(args.warmup)
     sync(det)
     det.profile(False)
     wprof = {k: v for k, v in det.profile_read().items() if k in abytes}
@@ -622,16 +689,17 @@ def main(args):
     det.profile_only(dom)
     det.profile(True)
     sync(det)
+    ties["raised"] = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    last = run_steps(args.steps)
     sync(det)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     det.profile(False)
     prof = det.profile_read()
-    gpu_host = out.to_host()           # the timed steps' outputs (checked against the oracle below)
+    gpu_host = last.to_host()          # the timed steps' outputs (checked against the oracle below)
+    ties_timed = dict(ties)
     elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
     # per-kernel table from a separate, untimed pass with every launch bracketed
     det.profile_only("")
@@ -851,8 +919,10 @@ def main(args):
         pick = sorted(set(np.linspace(0, F - 1, min(F, args.parity_files)).astype(int).tolist()))
         seeds = [seed0 + f for f in pick]
         outs, odt = oracle_outputs(args.mode, fs, n, seeds, params, th)
-        pr = compare_outputs([gpu_host[f] for f in pick], outs, exact_env=(args.mode == "reference"))
-        cnt = torch.tensor([pr["files"], pr["peaks_equal"], pr["troughs_equal"], pr["flags_equal"]],
+        pr = compare_outputs([gpu_host[f] for f in pick], outs, exact_env=(args.mode == "reference"), fs=fs,
+                             params=params)
+        cnt = torch.tensor([pr["files"], pr["peaks_equal"], pr["troughs_equal"], pr["flags_equal"],
+                            pr["ties_unresolved"], pr["ties_resolved"], ties_timed["raised"]],
                            dtype=torch.float64, device=cdev)
         worst = torch.tensor([pr["env_max_rel"], pr["floor_max_rel"]], dtype=torch.float64, device=cdev)
         dist.all_reduce(cnt)
@@ -860,8 +930,9 @@ def main(args):
         c, w = cnt.tolist(), worst.tolist()
         parity = {"files": int(c[0]), "ranks": world, "files_per_rank": len(pick), "peaks_equal": int(c[1]),
                   "troughs_equal": int(c[2]), "flags_equal": int(c[3]), "env_max_rel": w[0], "floor_max_rel": w[1],
-                  "env_tol": pr["env_tol"],
-                  "ok": c[1] == c[0] and c[2] == c[0] and c[3] == c[0] and max(w) <= pr["env_tol"]}
+                  "env_tol": pr["env_tol"], "ties_unresolved": int(c[4]), "ties_resolved": int(c[5]),
+                  "tie_flagged_in_timed_steps": int(c[6]),
+                  "ok": c[1] == c[0] and c[2] == c[0] and c[3] == c[0] and max(w) <= pr["env_tol"] and c[4] == 0}
         if rank == 0:
             cpu = {"value": len(pick) * n / odt, "unit": "audio-samples/s", "cores": th, "kind": "port",
                    "per_rank": True, "rank": 0, "affinity_cpus": aff, "os_cpu_count": ncpu,
@@ -967,6 +1038,11 @@ def main(args):
         if world == 1 and not args.no_cpu and args.cpu_files != 0:
             nfc = args.cpu_files if args.cpu_files > 0 else F
             cpu, parity = cpu_baseline(args.mode, fs, n, seed0, nfc, params, gpu_host)
+            # recordings the timed steps' tie check re-decided (summed over the
+            # steps; 0 on the synthetic batch: no decisive tie), and those left open
+            parity["tie_flagged_in_timed_steps"] = ties_timed["raised"]
+            parity["tie_check"] = ("every timed step: flags read back, tied recordings re-decided in numpy's "
+                                   "argsort order (engine.resolve_ties)")
         line = {
             "metric": METRIC, "value": value, "unit": "audio-samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,

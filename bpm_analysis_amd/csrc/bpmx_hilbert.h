@@ -41,6 +41,8 @@ struct HilbPlan {
     int32_t rd[HB_MAXS];           /* stage runs as Rader's 197-point DFT (hb_rader197) */
     int32_t nrtab;                 /* Rader tables after the prime tables: FFT_196(b) / 196 | W_196^e */
     int32_t per;                   /* rolling-mean outputs per thread, ceil(N / HB_T) */
+    int32_t cp[HB_MAXS];           /* > 0: small odd prime from exact constants (hb_radixp_const), cp groups */
+    int32_t cpo[HB_MAXS];          /* ... its rows' offset in HB_CP (bpmx_dft_consts.h) */
 };
 constexpr int HB_RD_P = 197;               /* Rader: 197 - 1 = 14 x 14, the 14-point DFTs as 2 x 7 prime-factor */
 
@@ -59,7 +61,7 @@ __global__ void k_hilbert_env(HilbArgs A, HilbPlan P);
 
 /* 1 and the plan, its tables and LDS size when Nd takes the fused kernel; 0 otherwise */
 int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes,
-                 bool mfma = true, bool rader = true);
+                 bool mfma = true, bool rader = true, bool cprime = true);
 
 }  // namespace bpmx
 

@@ -2170,7 +2170,10 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
             HIP_TRY(hipMemcpyAsync(d_tt2, ctx->nat_ttab.data(), ctx->nat_ttab.size() * 8, hipMemcpyHostToDevice, s));
             ctx->nat_ttab_dirty = false;
         }
-        a.ttab = std::getenv("BPMX_CARRY_SERIAL") ? nullptr : d_tt2;   /* (A/B: the serial tail) */
+        /* BPMX_CARRY_SERIAL (A/B diagnostic: the serial tail recursion) is read
+         * once per process, not on every run's launch path */
+        static const bool carry_serial = std::getenv("BPMX_CARRY_SERIAL") != nullptr;
+        a.ttab = carry_serial ? nullptr : d_tt2;
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
     }
     if (nt > 0) {

@@ -29,6 +29,7 @@
 #include "bpmx_hilbert.h"
 #include "bpmx_qsel.h"
 #include "bpmx_stamps.h"
+#include "bpmx_dft_consts.h"
 
 namespace bpmx {
 
@@ -182,6 +183,108 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, const HilbPlan &P, int
                     S.x[base + k * L] = r0[i][j];
                     if (k) S.x[base + (p - k) * L] = r1[i][j];
                 }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+/* Small odd-prime stages (p <= 29, hb_cp_off(p) >= 0) from exact constants
+ * (bpmx_dft_consts.h: correctly rounded cos / sin, laid out per frequency
+ * group and n in constant memory, so each step's row comes by scalar loads):
+ * no recurrence, no separate (a_n, b_n) pass.  Frequencies k = 0 .. h split
+ * into ng = ceil((h + 1) / HB_CP_G) groups; a wave takes one group
+ * (wave-uniform) for 64 butterflies, each lane one butterfly: per n it reads
+ * x_n, x_(p-n) (with the DIT's conjugate twiddles first), forms a_n, b_n in
+ * registers and accumulates A_k = sum a_n cos(2 pi n k / p),
+ * B_k = sum b_n sin(2 pi n k / p) over the group's k.  Results wait in
+ * registers for the barrier, then go back in place (with the DIF's
+ * twiddles).  One round of waves: the plan takes this form only when
+ * ng ceil((M / p) / 64) <= HB_T / 64. */
+__host__ __device__ constexpr int hb_cp_ng(int p) { return ((p + 1) / 2 + HB_CP_G - 1) / HB_CP_G; }
+
+template <bool INV>
+__device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &PL, int si) {
+    constexpr int G = HB_CP_G;
+    const int M = PL.M, B = PL.B[si], L = PL.L[si], p = PL.rad[si], h = (p - 1) >> 1;
+    const uint64_t dL = PL.dL[si];
+    const int nbf = hb_div(M, PL.dP[si]), step = PL.N / B, nbw = (nbf + 63) >> 6;
+    const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const int g = __builtin_amdgcn_readfirstlane(wv / nbw);                 /* wave-uniform group */
+    const int bf = (wv - g * nbw) * 64 + lane;
+    const bool act = g < PL.cp[si] && bf < nbf;                           /* cp[si] = ng */
+    double2 r0[G], r1[G];
+    int base = 0, n2 = 0;
+    if (act) {
+        const int blk = hb_div(bf, dL);
+        n2 = bf - blk * L;
+        base = blk * B + n2;
+        double ax[G], ay[G], bx[G], by[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) ax[j] = ay[j] = bx[j] = by[j] = 0.0;
+        const double *row = HB_CP + PL.cpo[si] + g * (h * 2 * G);
+        /* the DIT's input twiddles w^(e n) and w^(e (p - n)), e = step n2, by
+         * products from two table values: t_n = t_(n-1) w^e, t_(p-n) =
+         * w^(e p) conj(t_n) (lanes' table indices step n2 k are strided, so
+         * every per-output table read was a bank-conflicted pair of LDS reads) */
+        const double2 w1 = (INV && n2) ? S.tw(step * n2) : make_double2(1.0, 0.0);
+        const double2 wp = (INV && n2) ? S.tw(step * n2 * p) : make_double2(1.0, 0.0);
+        double2 tn = w1;
+        /* each step's two LDS reads are issued a step ahead */
+        double2 un = S.x[base + L], vn = S.x[base + (p - 1) * L];
+#pragma unroll 1
+        for (int n = 1; n <= h; ++n, row += 2 * G) {
+            double2 u = un, v = vn;
+            if (n < h) {
+                un = S.x[base + (n + 1) * L];
+                vn = S.x[base + (p - n - 1) * L];
+            }
+            if (INV && n2) {
+                u = cmulc(u, tn);
+                v = cmulc(v, cmulc(wp, tn));
+                tn = cmul(tn, w1);
+            }
+            const double2 a = cadd(u, v), b = csub(u, v);
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const double c = row[j], sn = row[G + j];
+                ax[j] = __builtin_fma(a.x, c, ax[j]);
+                ay[j] = __builtin_fma(a.y, c, ay[j]);
+                bx[j] = __builtin_fma(b.x, sn, bx[j]);
+                by[j] = __builtin_fma(b.y, sn, by[j]);
+            }
+        }
+        const double2 x0 = S.x[base];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            /* forward: X_k = x0 + A - iB, X_(p-k) = x0 + A + iB; inverse: signs swapped */
+            const double2 xa = make_double2(x0.x + ax[j], x0.y + ay[j]);
+            const double2 mib = INV ? make_double2(-by[j], bx[j]) : make_double2(by[j], -bx[j]);
+            r0[j] = cadd(xa, mib);
+            r1[j] = csub(xa, mib);
+        }
+    }
+    /* the DIF's output twiddles likewise: t_k from w^(e k0) by products with
+     * w^e, t_(p-k) = w^(e p) conj(t_k) */
+    double2 w1 = make_double2(1.0, 0.0), wp = w1, tk = w1;
+    if (!INV && act && n2) {
+        w1 = S.tw(step * n2);
+        wp = S.tw(step * n2 * p);
+        tk = S.tw(step * n2 * g * G);
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int k = g * G + j;
+            if (k > h) break;
+            if (!INV && n2) {
+                S.x[base + k * L] = k ? cmul(r0[j], tk) : r0[j];
+                if (k) S.x[base + (p - k) * L] = cmul(r1[j], cmulc(wp, tk));
+                tk = cmul(tk, w1);
+            } else {
+                S.x[base + k * L] = r0[j];
+                if (k) S.x[base + (p - k) * L] = r1[j];
             }
         }
     }
@@ -474,6 +577,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     for (int i = r2 ? 1 : 0; i < P.ns; ++i) {
         if (P.rad[i] == 2) hb_radix2<false>(S, P, i);
         else if (P.rd[i]) hb_rader197<false>(S, P, S.pt + P.nptab);
+        else if (P.cp[i]) hb_radixp_const<false>(S, P, i);
         else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<false, true>(S, P, i, S.pt + P.ptab[i]);
         else if (P.mf[i]) hb_radixp_mfma<false, false>(S, P, i, S.pt + P.ptab[i]);
         else hb_radixp<false>(S, P, i, S.pt + P.ptab[i]);
@@ -502,6 +606,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     for (int i = P.ns - 1; i >= (r2 ? 1 : 0); --i) {
         if (P.rad[i] == 2) hb_radix2<true>(S, P, i);
         else if (P.rd[i]) hb_rader197<true>(S, P, S.pt + P.nptab);
+        else if (P.cp[i]) hb_radixp_const<true>(S, P, i);
         else if (P.mf[i] && P.L[i] == 1) hb_radixp_mfma<true, true>(S, P, i, S.pt + P.ptab[i]);
         else if (P.mf[i]) hb_radixp_mfma<true, false>(S, P, i, S.pt + P.ptab[i]);
         else hb_radixp<true>(S, P, i, S.pt + P.ptab[i]);
@@ -551,23 +656,32 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         /* window of output i: [max(i + offw - w, 0), min(i + offw, N)) */
         auto we = [&](int i) { return min(i + offw, N); };
         auto ws = [&](int i) { return max(i + offw - wi, 0); };
-        double ad[HB_RMPER], sb[HB_RMPER];
-#pragma unroll
-        for (int j = 1; j < HB_RMPER; ++j) {
-            const int i = i0 + j;
-            ad[j] = (j < cnt && we(i) > we(i - 1)) ? mag[we(i) - 1] : 0.0;
-            sb[j] = (j < cnt && ws(i) > ws(i - 1)) ? mag[ws(i - 1)] : 0.0;
-        }
         double sum = 0.0;
         for (int q = ws(i0); q < we(i0); ++q) sum += mag[q];
         ev[0] = mean(sum, we(i0) - ws(i0));
+        /* in two halves, each half's reads issued before its sums (all of them
+         * at once held 40 more doubles beside ev and spilled) */
+        constexpr int HALF = HB_RMPER / 2;
 #pragma unroll
-        for (int j = 1; j < HB_RMPER; ++j)
-            if (j < cnt) {
-                sum += ad[j];
-                sum -= sb[j];
-                ev[j] = mean(sum, we(i0 + j) - ws(i0 + j));
+        for (int c0 = 1; c0 < HB_RMPER; c0 += HALF) {
+            double ad[HALF], sb[HALF];
+#pragma unroll
+            for (int u = 0; u < HALF; ++u) {
+                const int j = c0 + u, i = i0 + j;
+                ad[u] = (j < HB_RMPER && j < cnt && we(i) > we(i - 1)) ? mag[we(i) - 1] : 0.0;
+                sb[u] = (j < HB_RMPER && j < cnt && ws(i) > ws(i - 1)) ? mag[ws(i - 1)] : 0.0;
             }
+#pragma unroll
+            for (int u = 0; u < HALF; ++u) {
+                const int j = c0 + u;
+                if (j < HB_RMPER && j < cnt) {
+                    sum += ad[u];
+                    sum -= sb[u];
+                    ev[j] = mean(sum, we(i0 + j) - ws(i0 + j));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     STAMP(8);
     /* through LDS, so the global stores are coalesced */
@@ -600,7 +714,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
 /* ---------------------------------------------------------------------- */
 /* host: plan + tables (long double), cached per N */
 int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs, size_t *lds_bytes, bool mfma,
-                 bool rader) {
+                 bool rader, bool cprime) {
     if (nd < 4 || (nd & 1)) return 0;
     const int64_t M = nd / 2;
     int rad[HB_MAXS], ns = 0;
@@ -646,8 +760,14 @@ int hilbert_plan(int64_t nd, int window, HilbPlan *P, std::vector<double2> *tabs
             /* Rader's 197-point DFT on the contiguous, twiddle-free stage */
             P->rd[i] = rader && r == HB_RD_P && P->L[i] == 1;
             if (P->rd[i]) P->mf[i] = 0;
+            /* small primes with compile-time constants, one round of waves */
+            const bool cp = cprime && hb_cp_off(r) >= 0 && !P->rd[i] &&
+                            (int64_t)hb_cp_ng(r) * ((M / r + 63) / 64) <= (int64_t)(HB_T / 64);
+            P->cp[i] = cp ? hb_cp_ng(r) : 0;
+            P->cpo[i] = cp ? hb_cp_off(r) : 0;
+            if (cp) P->mf[i] = 0;
             /* register-held outputs: (M / p) ceil((h + 1) / HB_KB) tasks over HB_T threads */
-            if (!P->mf[i] && !P->rd[i] && (M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT)
+            if (!P->mf[i] && !P->rd[i] && !P->cp[i] && (M / r) * (((r + 1) / 2 + HB_KB - 1) / HB_KB) > (int64_t)HB_T * HB_MAXT)
                 return 0;
             int off = -1, acc = 0;
             for (int q : primes) { if (q == r) off = acc; acc += q; }

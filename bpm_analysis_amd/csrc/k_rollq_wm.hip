@@ -458,6 +458,7 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
     /* LDS, sort phase: posA[m8] | posB[m8] | kh[m8] | cnt[NWV][128] (two 16-bit counters per word).
      * Slots >= m are padding: they sort last, so they are neither stored nor counted. */
     const int IT = (m + WM_T - 1) / WM_T;                    /* rounds per wave */
+    const int mu = __builtin_amdgcn_readfirstlane(m), ITu = __builtin_amdgcn_readfirstlane(IT);
     const int S = 64 * IT;                                   /* slots per wave */
     const int m8 = (m + 7) & ~7;
     uint16_t *posA = (uint16_t *)(smem + Lay.area);
@@ -532,18 +533,24 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             for (int j = lane; j < 128; j += 64) wc[j] = 0;
             /* digits of all this lane's items first (independent LDS reads) */
             uint32_t dg8[(MAXIT + 3) / 4], rk16[(MAXIT + 1) / 2];   /* packed: digit 8 b, rank 16 b */
+            /* m and IT opaque per loop: otherwise the per-item masks of the three
+             * unrolled loops are hoisted out of the digit loop and live in ~100
+             * SGPRs, which spill to VGPR lanes (a readlane per use) */
+            int mo = mu, ITo = ITu, sb = wid * S + lane;
+            asm volatile("" : "+s"(mo), "+s"(ITo), "+v"(sb));
 #pragma unroll
             for (int i = 0; i < MAXIT; ++i) {
-                const int slot = wid * S + i * 64 + lane;
-                const uint32_t dg = (i < IT && slot < m) ? (kh[posA[slot]] >> sh) & 0xFFu : 0u;
+                const int slot = sb + i * 64;
+                const uint32_t dg = (i < ITo && slot < mo) ? (kh[posA[slot]] >> sh) & 0xFFu : 0u;
                 if ((i & 3) == 0) dg8[i >> 2] = dg; else dg8[i >> 2] |= dg << (8 * (i & 3));
             }
             __builtin_amdgcn_wave_barrier();
+            asm volatile("" : "+s"(mo), "+s"(ITo), "+v"(sb));
 #pragma unroll
             for (int i = 0; i < MAXIT; ++i) {
-                if (i < IT) {
-                    const int slot = wid * S + i * 64 + lane;
-                    const bool valid = slot < m;
+                if (i < ITo) {
+                    const int slot = sb + i * 64;
+                    const bool valid = slot < mo;
                     const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
                     uint64_t peers;
                     if (wbin_all) {                          /* uniform */
@@ -600,10 +607,11 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
             __syncthreads();
             STAMP(2);
             const uint16_t *c16 = (const uint16_t *)cnt;
+            asm volatile("" : "+s"(mo), "+s"(ITo), "+v"(sb));
 #pragma unroll
             for (int i = 0; i < MAXIT; ++i) {
-                const int slot = wid * S + i * 64 + lane;
-                if (i < IT && slot < m) {
+                const int slot = sb + i * 64;
+                if (i < ITo && slot < mo) {
                     const uint32_t dg = (dg8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
                     const uint32_t rnk = (rk16[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
                     posB[(int)c16[(wid * 128 + (dg >> 1)) * 2 + (dg & 1)] + (int)rnk] = posA[slot];
@@ -962,6 +970,8 @@ __device__ __forceinline__ void rollq_wm_run(const RollqArgs &a, int32_t *full, 
  * per-recording decisions.  (The full draft before sanitize stays a launch of
  * its own: a second rolling-quantile call site in this kernel spills.)
  * ------------------------------------------------------------------------- */
+static_assert(WM_T == QR_T && WM_MMAX <= QR_MAX,
+              "k_floor_wm runs qr_select with its own threads over up to WM_MMAX samples");
 __global__ __launch_bounds__(WM_T) void k_floor_wm(FloorWmArgs A) {
     __shared__ RqShared sh;
     __shared__ int s_sc[WM_T / 64 + 1];

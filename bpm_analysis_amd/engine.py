@@ -77,6 +77,8 @@ class Result:
         out = []
         for f in range(self.n_files):
             a, b = int(self.doff[f]), int(self.doff[f + 1])
+            if flags[f] & N.F_TOO_SHORT:
+                b = a           # no outputs (include/bpmx.h): empty slices, not the buffers' old contents
             out.append(dict(
                 sr=self.sr, env=env[a:b], floor=None if floor is None else floor[a:b],
                 y=None if y is None else y[a:b],
@@ -193,7 +195,7 @@ class Detector:
                                                 ctypes.byref(order), self.stream_handle()), "bpmx_run_ordered")
         return out
 
-    def resolve_ties(self, out: Result, params: dict, stages: int = N.STAGE_ALL) -> int:
+    def resolve_ties(self, out: Result, params: dict, stages: int = N.STAGE_ALL, options: int = 0) -> int:
         """Re-decide find_peaks' distance filter in numpy's own argsort order for
         the recordings of `out` that carry a decisive-tie bit (F_TROUGH_TIE /
         F_PEAK_TIE), so their troughs, floor and raw peaks are the reference's
@@ -209,8 +211,11 @@ class Detector:
         candidates, whose order is taken after.  The flagged recordings run as a
         sub-batch (ds = 1, envelopes gathered on the device); their results are
         written back into `out` and their flags carry F_*_ORDERED instead of
-        F_*_TIE.  Returns the number of recordings re-run (0: nothing to do, no
-        launch).  Synchronises the current stream."""
+        F_*_TIE.  `options`: the run's bpmx_option bits, forwarded to the
+        sub-batch runs (BPMX_OPT_STATS, which bpmx_run_ordered rejects, masked
+        off) so they take the same floor kernels as the original run.  Returns
+        the number of recordings re-run (0: nothing to do, no launch).
+        Synchronises the current stream."""
         torch = _torch()
         det_st = stages & (N.STAGE_FLOOR | N.STAGE_PEAKS)
         bits = (N.F_TROUGH_TIE if det_st & N.STAGE_FLOOR else 0) | (N.F_PEAK_TIE if det_st & N.STAGE_PEAKS else 0)
@@ -258,7 +263,8 @@ class Detector:
             rank[s].copy_(torch.from_numpy(r))
             use[s].copy_(torch.from_numpy(u))
 
-        run = lambda st, o: self.run(None, fo, d.sr, params, stages=st, out=sub, d=d, order=o)
+        opts = options & ~N.OPT_STATS
+        run = lambda st, o: self.run(None, fo, d.sr, params, stages=st, out=sub, d=d, order=o, options=opts)
         ranked = set()
         if det_st & N.STAGE_FLOOR and (flags[sel] & N.F_TROUGH_TIE).any():
             run(det_st, order({0}, ()))
@@ -282,6 +288,31 @@ class Detector:
             out.n_peaks[sel] = sub.n_peaks
         out.flags[torch.from_numpy(sel).to(dev)] = torch.from_numpy(fl).to(dev)
         return F
+
+    def tie_check_start(self, out: Result):
+        """Start the flags read-back that ``tie_check_finish`` decides on: an
+        asynchronous copy of ``out.flags`` into pinned host memory and an event
+        behind it on the current stream, so the host need not wait for the run
+        before queuing the next one (a batch pipeline keeps two ``Result`` sets
+        and checks run k while run k + 1 is queued)."""
+        torch = _torch()
+        host = torch.empty(out.flags.shape, dtype=out.flags.dtype, pin_memory=True)
+        host.copy_(out.flags, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return host, ev
+
+    def tie_check_finish(self, handle, out: Result, params: dict, stages: int = N.STAGE_ALL,
+                         options: int = 0) -> int:
+        """Wait for the read-back ``tie_check_start`` began; if any recording of
+        `out` carries a decisive-tie bit, re-decide them (``resolve_ties``: a
+        launch and a host sort only then).  Returns the recordings re-run."""
+        host, ev = handle
+        ev.synchronize()
+        bits = N.F_TROUGH_TIE | N.F_PEAK_TIE
+        if not (host.numpy() & bits).any():
+            return 0
+        return self.resolve_ties(out, params, stages, options)
 
     def synth(self, frame_offsets: Sequence[int], fs: int, channels: int = 1, seed0: int = 0,
               seeds: Optional[Sequence[int]] = None):
@@ -367,7 +398,7 @@ class Detector:
             res = self.run(pcm, fo, fs, params, mode=mode, stages=stages, channels=ch, want_y=want_y, log=log,
                            options=options)
             if resolve_ties:
-                self.resolve_ties(res, params, stages)
+                self.resolve_ties(res, params, stages, options)
             out = res.to_host()          # .cpu() waits for this stream only
             self.host_stream().synchronize()
         return out
@@ -387,7 +418,7 @@ class Detector:
                 out.floor.copy_(torch.from_numpy(np.concatenate(floors).astype(np.float64)).to(self.device))
             self.run(None, fo, d.sr, params, stages=stages, out=out, d=d, options=options)
             if resolve_ties:
-                self.resolve_ties(out, params, stages)
+                self.resolve_ties(out, params, stages, options)
             res = out.to_host()
             self.host_stream().synchronize()
         return res

@@ -156,7 +156,11 @@ typedef struct {
 typedef struct {
     int32_t n_files;
     int32_t reserved;
-    const void *pcm;              /* device: frames of all files back to back, interleaved channels */
+    const void *pcm;              /* device: frames of all files back to back, interleaved channels.
+                                     The library may read from the 16-byte boundary at or below pcm
+                                     (an int16 base a whole number of frames past it is read from
+                                     there; the bytes before pcm are read and discarded, never used),
+                                     so that a recording's outputs do not depend on its alignment */
     const int64_t *frame_offsets; /* host: n_files+1 frame offsets into pcm */
 } bpmx_batch;
 

@@ -15,13 +15,14 @@
 using namespace bpmx;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> &y, std::vector<double> &env_out) {
+static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> &y, std::vector<double> &env_out,
+                  bool cprime = true) {
     HilbPlan P;
     std::vector<double2> tabs;
     size_t lds = 0;
-    if (!hilbert_plan(nd, 30, &P, &tabs, &lds, mfma, rader)) { printf("no plan\n"); exit(1); }
+    if (!hilbert_plan(nd, 30, &P, &tabs, &lds, mfma, rader, cprime)) { printf("no plan\n"); exit(1); }
     printf("nd %lld M %d stages", (long long)nd, P.M);
-    for (int i = 0; i < P.ns; ++i) printf(" %d%s", P.rad[i], P.mf[i] ? "(mfma)" : P.rd[i] ? "(rader)" : "");
+    for (int i = 0; i < P.ns; ++i) printf(" %d%s", P.rad[i], P.mf[i] ? "(mfma)" : P.rd[i] ? "(rader)" : P.cp[i] ? "(const)" : "");
     printf(" lds %zu\n", lds);
     std::vector<int64_t> doff(F + 1);
     for (int f = 0; f <= F; ++f) doff[f] = (int64_t)f * nd;
@@ -69,17 +70,19 @@ int main(int argc, char **argv) {
     std::vector<double> y((size_t)F * nd);
     unsigned long long s = 1;
     for (auto &v : y) { s = s * 6364136223846793005ull + 1442695040888963407ull; v = (double)(s >> 11) / 9007199254740992.0 - 0.5; }
-    std::vector<double> e0, e1, e2;
-    run(F, nd, false, false, y, e0);
-    run(F, nd, true, false, y, e1);
-    run(F, nd, true, true, y, e2);
-    double mx = 0, d = 0, d2 = 0;
+    std::vector<double> e0, e1, e2, e3;
+    run(F, nd, false, false, y, e0, false);
+    run(F, nd, true, false, y, e1, false);
+    run(F, nd, true, true, y, e2, false);
+    run(F, nd, true, true, y, e3, true);
+    double mx = 0, d = 0, d2 = 0, d3 = 0;
     for (size_t i = 0; i < e0.size(); ++i) {
         mx = fmax(mx, fabs(e0[i]));
         d = fmax(d, fabs(e0[i] - e1[i]));
         d2 = fmax(d2, fabs(e0[i] - e2[i]));
+        d3 = fmax(d3, fabs(e0[i] - e3[i]));
     }
-    printf("max |env_direct - env_mfma| / max|env| = %.3e, max |env_direct - env_rader| / max|env| = %.3e\n", d / mx,
-           d2 / mx);
+    printf("max |env_direct - env_X| / max|env|: mfma %.3e, rader %.3e, rader + const primes %.3e\n", d / mx,
+           d2 / mx, d3 / mx);
     return 0;
 }
