@@ -653,6 +653,25 @@ static int run_impl(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
     /* long recordings' quantiles: radix select over many workgroups (k_ql_*) */
     auto quantile_long = [&](const QuantArgs &q) -> int {
         int qrc = BPMX_OK;
+#ifndef BPMX_QL_RADIX
+        /* five launches, two passes over env (k_qv_*, r06) */
+        QvArgs V;
+        V.Q = q;
+        V.boff = d_boff; V.bmax = bmax; V.bmin = bmin;
+        V.rg = (QvRange *)ctx->buf("qv_range", (size_t)F * sizeof(QvRange), &qrc);
+        V.st = (QvState *)ctx->buf("qv_state", (size_t)F * Q_SLOTS * sizeof(QvState), &qrc);
+        V.hist = (unsigned int *)ctx->buf("qv_hist", (size_t)F * QV_BINS * 4, &qrc);
+        V.cand = (unsigned long long *)ctx->buf("qv_cand", (size_t)sumnd * Q_SLOTS * 8, &qrc);
+        if (qrc != BPMX_OK) return qrc;
+        HIP_TRY(hipMemsetAsync(V.hist, 0, (size_t)F * QV_BINS * 4, s));
+        const dim3 gv((unsigned)((maxnd + QV_CHUNK - 1) / QV_CHUNK), (unsigned)F);
+        LAUNCH(ctx, s, "k_quantile", k_qv_range, dim3(F), dim3(64), 0, s, V);
+        LAUNCH(ctx, s, "k_quantile", k_qv_hist, gv, dim3(256), 0, s, V);
+        LAUNCH(ctx, s, "k_quantile", k_qv_select, dim3(F, q.n_levels), dim3(256), 0, s, V);
+        LAUNCH(ctx, s, "k_quantile", k_qv_collect, gv, dim3(256), 0, s, V);
+        LAUNCH(ctx, s, "k_quantile", k_qv_final, dim3(F, q.n_levels), dim3(256), 0, s, V);
+        return BPMX_OK;
+#endif
         QlArgs A;
         A.Q = q;
         A.st = (QlState *)ctx->buf("ql_state", (size_t)F * Q_SLOTS * sizeof(QlState), &qrc);

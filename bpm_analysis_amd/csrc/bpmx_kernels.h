@@ -100,6 +100,39 @@ struct QlArgs {
     unsigned int *hist;     /* [QL_PASSES][F][Q_SLOTS][QL_BINS] (zeroed before pass 0) */
     int32_t pass;
 };
+/* The same quantiles in five launches and two passes over env (k_detect.hip,
+ * r06): bins of the order-preserving key over the recording's own key range
+ * (k_qv_range, from the block max/min tables), one histogram for all levels
+ * (k_qv_hist), the target bin and the rank inside it per level (k_qv_select),
+ * the target bin's keys gathered per level plus the least key above it
+ * (k_qv_collect), the exact order statistics among the gathered keys by a
+ * radix select and numpy's _lerp (k_qv_final). */
+constexpr int QV_BITS = 13, QV_BINS = 1 << QV_BITS, QV_CHUNK = 32768;
+struct QvRange {
+    unsigned long long kmin;
+    int32_t shift, pad;
+};
+struct QvState {
+    long long lo;                 /* the order statistic's rank floor((n - 1) q) */
+    long long r;                  /* its rank inside the target bin */
+    unsigned long long next;      /* least key in a bin above the target (atomicMin) */
+    int32_t bin, top;             /* target bin; q reaches n - 1 */
+    uint32_t cnt, cbin;           /* keys gathered; the target bin's count */
+};
+struct QvArgs {
+    QuantArgs Q;
+    const int64_t *boff;          /* block-table offsets (k_block_stats) */
+    const double *bmax, *bmin;
+    QvRange *rg;                  /* [F] */
+    QvState *st;                  /* [F][Q_SLOTS] */
+    unsigned int *hist;           /* [F][QV_BINS] (zeroed) */
+    unsigned long long *cand;     /* level l of recording f at (doff[f] * Q_SLOTS + l * n_f): room for every key */
+};
+__global__ void k_qv_range(QvArgs A);
+__global__ void k_qv_hist(QvArgs A);
+__global__ void k_qv_select(QvArgs A);
+__global__ void k_qv_collect(QvArgs A);
+__global__ void k_qv_final(QvArgs A);
 __global__ void k_ql_init(QlArgs A);
 __global__ void k_ql_hist(QlArgs A);
 __global__ void k_ql_select(QlArgs A);

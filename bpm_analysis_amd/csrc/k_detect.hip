@@ -176,6 +176,210 @@ __global__ __launch_bounds__(64) void k_ql_final(QlArgs A) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* Long recordings' quantiles in two passes over env (r06; k_ql_* took six
+ * digit passes, a "next" pass and fifteen launches).  Bins are the
+ * order-preserving key's offset from the recording's least finite value's key,
+ * shifted so the recording's range spans at most QV_BINS bins, clamped at both
+ * ends: monotone in the key for every input (NaN and infinite keys clamp to an
+ * end), so the r-th smallest key lies in the bin where the cumulative count
+ * passes r, at rank r - (count below) inside it.  The bins adapt to the
+ * recording, so the target bin holds few keys on real envelopes (a skewed one
+ * only makes the last step longer). */
+namespace {
+__device__ __forceinline__ int qv_bin(uint64_t k, const QvRange &g) {
+    if (k <= g.kmin) return 0;
+    const uint64_t d = (k - g.kmin) >> g.shift;
+    return d >= (uint64_t)QV_BINS ? QV_BINS - 1 : (int)d;
+}
+}  // namespace
+
+/* per recording: key range from the block tables, and each level's rank */
+__global__ __launch_bounds__(64) void k_qv_range(QvArgs A) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    if (!ql_sel(A.Q, f)) return;
+    const int64_t b0 = A.boff[f], nb = A.boff[f + 1] - b0;
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    for (int64_t b = lane; b < nb; b += 64) {
+        mn = fmin(mn, A.bmin[b0 + b]);
+        mx = fmax(mx, A.bmax[b0 + b]);
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) {
+        QvRange g;
+        g.pad = 0;
+        if (!(mn <= mx)) {                                    /* no finite value: bins by the key's top bits */
+            g.kmin = 0;
+            g.shift = 64 - QV_BITS;
+        } else {
+            g.kmin = f64_key(mn);
+            const uint64_t span = f64_key(mx) - g.kmin;
+            const int bits = span ? 64 - __clzll((long long)span) : 0;
+            g.shift = bits > QV_BITS ? bits - QV_BITS : 0;
+        }
+        A.rg[f] = g;
+    }
+    const int64_t n = A.Q.doff[f + 1] - A.Q.doff[f];
+    if (lane < A.Q.n_levels) {
+        const double vi = (double)(n - 1) * A.Q.q[lane];
+        QvState s;
+        s.top = vi >= (double)(n - 1);
+        s.lo = s.top ? (long long)(n - 1) : (long long)floor(vi);
+        s.r = 0; s.next = ~0ull; s.bin = 0; s.cnt = 0; s.cbin = 0;
+        A.st[(int64_t)f * Q_SLOTS + lane] = s;
+    }
+}
+
+/* one histogram of the bins per recording (every level shares it) */
+__global__ __launch_bounds__(256) void k_qv_hist(QvArgs A) {
+    const int f = blockIdx.y;
+    if (!ql_sel(A.Q, f)) return;
+    const int64_t d0 = A.Q.doff[f], n = A.Q.doff[f + 1] - d0;
+    const int64_t c0 = (int64_t)blockIdx.x * QV_CHUNK;
+    if (c0 >= n) return;
+    const int64_t c1 = min<int64_t>(n, c0 + QV_CHUNK);
+    __shared__ unsigned int hist[QV_BINS];
+    for (int i = threadIdx.x; i < QV_BINS; i += 256) hist[i] = 0u;
+    const QvRange g = A.rg[f];
+    __syncthreads();
+    const double *x = A.Q.env + d0;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) atomicAdd(&hist[qv_bin(f64_key(x[i]), g)], 1u);
+    __syncthreads();
+    unsigned int *gh = A.hist + (int64_t)f * QV_BINS;
+    for (int i = threadIdx.x; i < QV_BINS; i += 256) {
+        const unsigned int c = hist[i];
+        if (c) atomicAdd(&gh[i], c);
+    }
+}
+
+/* per (recording, level): the bin where the cumulative count passes the rank */
+__global__ __launch_bounds__(256) void k_qv_select(QvArgs A) {
+    const int f = blockIdx.x, l = blockIdx.y;
+    if (!ql_sel(A.Q, f) || l >= A.Q.n_levels) return;
+    const unsigned int *gh = A.hist + (int64_t)f * QV_BINS;
+    QvState *ps = A.st + (int64_t)f * Q_SLOTS + l;
+    const long long r = ps->lo;
+    __shared__ int sh[256 / 64 + 1];
+    constexpr int PER = QV_BINS / 256;                          /* consecutive bins per thread */
+    unsigned int c[PER];
+    int sum = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) { c[u] = gh[threadIdx.x * PER + u]; sum += (int)c[u]; }
+    int tot;
+    const long long before = block_scan_int<256>(sum, sh, &tot);
+    if (before <= r && r < before + sum) {                       /* exactly one thread */
+        long long rr = r - before;
+        int d = 0;
+        while (rr >= (long long)c[d]) { rr -= c[d]; ++d; }
+        ps->bin = threadIdx.x * PER + d;
+        ps->r = rr;
+        ps->cbin = c[d];
+    }
+}
+
+/* the target bins' keys, per level, and the least key above each target bin */
+__global__ __launch_bounds__(256) void k_qv_collect(QvArgs A) {
+    const int f = blockIdx.y;
+    if (!ql_sel(A.Q, f)) return;
+    const int64_t d0 = A.Q.doff[f], n = A.Q.doff[f + 1] - d0;
+    const int64_t c0 = (int64_t)blockIdx.x * QV_CHUNK;
+    if (c0 >= n) return;
+    const int64_t c1 = min<int64_t>(n, c0 + QV_CHUNK);
+    const int L = A.Q.n_levels, lane = lane_id();
+    const QvRange g = A.rg[f];
+    __shared__ int s_tb[Q_SLOTS];
+    if (threadIdx.x < L) s_tb[threadIdx.x] = A.st[(int64_t)f * Q_SLOTS + threadIdx.x].bin;
+    __syncthreads();
+    int tb[Q_SLOTS];
+    unsigned long long mn[Q_SLOTS];
+#pragma unroll
+    for (int l = 0; l < Q_SLOTS; ++l) { tb[l] = l < L ? s_tb[l] : QV_BINS; mn[l] = ~0ull; }
+    const double *x = A.Q.env + d0;
+    unsigned long long *cb = A.cand + d0 * Q_SLOTS;
+    for (int64_t i0 = c0; i0 < c1; i0 += 256) {                 /* uniform trip count: ballots inside */
+        const int64_t i = i0 + threadIdx.x;
+        const bool in = i < c1;
+        const uint64_t k = in ? f64_key(x[i]) : 0ull;
+        const int b = in ? qv_bin(k, g) : -1;
+#pragma unroll
+        for (int l = 0; l < Q_SLOTS; ++l) {
+            if (l >= L) continue;
+            const bool hit = b == tb[l];
+            if (b > tb[l] && k < mn[l]) mn[l] = k;
+            const uint64_t bal = __ballot(hit);
+            if (bal) {                                           /* one counter atomic per wave and level */
+                unsigned int base = 0;
+                if (lane == __ffsll((long long)bal) - 1)
+                    base = atomicAdd(&A.st[(int64_t)f * Q_SLOTS + l].cnt, (unsigned int)__popcll(bal));
+                base = (unsigned int)__shfl((int)base, __ffsll((long long)bal) - 1);
+                if (hit) cb[(int64_t)l * n + base + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+            }
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < Q_SLOTS; ++l) {
+        if (l >= L) continue;
+        unsigned long long m = mn[l];
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long om = __shfl_xor(m, o);
+            m = om < m ? om : m;
+        }
+        if (lane == 0 && m != ~0ull) atomicMin(&A.st[(int64_t)f * Q_SLOTS + l].next, m);
+    }
+}
+
+/* per (recording, level): the r-th and (r+1)-th smallest of the gathered keys
+ * by an 8-bit radix select over them (L2-resident: a few hundred keys on the
+ * C5 envelopes), the (r+1)-th from the bins above when the bin ends at r;
+ * then numpy's _lerp as k_ql_final */
+__global__ __launch_bounds__(256) void k_qv_final(QvArgs A) {
+    const int f = blockIdx.x, l = blockIdx.y;
+    if (!ql_sel(A.Q, f) || l >= A.Q.n_levels) return;
+    const int64_t d0 = A.Q.doff[f], n = A.Q.doff[f + 1] - d0;
+    const QvState st = A.st[(int64_t)f * Q_SLOTS + l];
+    const unsigned long long *cb = A.cand + d0 * Q_SLOTS + (int64_t)l * n;
+    const long long c = st.cnt;
+    __shared__ unsigned int hist[256];
+    __shared__ unsigned long long s_pre;
+    __shared__ long long s_rank;
+    auto select = [&](long long rank) -> unsigned long long {
+        unsigned long long prefix = 0ull, mask = 0ull;
+        for (int pass = 0; pass < 8; ++pass) {
+            const int shf = 56 - 8 * pass;
+            hist[threadIdx.x] = 0u;
+            __syncthreads();
+            for (long long i = threadIdx.x; i < c; i += 256) {
+                const unsigned long long k = cb[i];
+                if ((k & mask) == prefix) atomicAdd(&hist[(k >> shf) & 255u], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                long long rr = rank;
+                int d = 0;
+                while (d < 255 && rr >= (long long)hist[d]) { rr -= hist[d]; ++d; }
+                s_pre = prefix | ((unsigned long long)d << shf);
+                s_rank = rr;
+            }
+            __syncthreads();
+            prefix = s_pre;
+            rank = s_rank;
+            mask |= 0xFFull << shf;
+            __syncthreads();
+        }
+        return prefix;
+    };
+    const unsigned long long ka = select(st.r);
+    double res = key_f64(ka);
+    if (!st.top) {
+        const unsigned long long kb = st.r + 1 < c ? select(st.r + 1) : st.next;
+        res = np_lerp(res, key_f64(kb), (double)(n - 1) * A.Q.q[l] - (double)st.lo);
+    }
+    if (threadIdx.x == 0)
+        for (int s = 0; s < Q_SLOTS; ++s)
+            if ((A.Q.slot[l] >> s) & 1) A.Q.qv[(int64_t)f * Q_SLOTS + s] = res;
+}
+
+/* ------------------------------------------------------------------------ */
 __global__ __launch_bounds__(256) void k_block_stats(BlockStatArgs A) {
     const int f = blockIdx.x;
     if (f >= A.n_files || !A.active[f]) return;

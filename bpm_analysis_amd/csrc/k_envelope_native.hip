@@ -563,11 +563,16 @@ __global__ __launch_bounds__(64 * NM_WAVES, NM_MINW) void k_native_blocks_mfma(N
     const int64_t clast = (total & ~(int64_t)7) - 8;
     auto dma = [&](int64_t s0, u4 *slot) {
         const int64_t a0 = s0 & ~(int64_t)7;
+        /* the chunk count opaque here: otherwise the per-r lane masks
+         * (q < nch) are hoisted out of the tile loop into ~36 SGPRs, which
+         * spill, and every refill pays a readlane per mask */
+        int nchv = nch, lanev = lane;
+        asm volatile("" : "+s"(nchv), "+v"(lanev));
 #pragma unroll
         for (int r = 0; r < NM_NDMA; ++r) {
-            const int q = r * 64 + lane;
+            const int q = r * 64 + lanev;
             int64_t c = a0 + (int64_t)q * 8;
-            c = (q < nch && c + 8 <= total) ? c : clast;
+            c = (q < nchv && c + 8 <= total) ? c : clast;
             /* inline asm, not __builtin_amdgcn_global_load_lds: the compiler cannot
              * tell the slots apart and would put a vmcnt(0) before the next LDS
              * read, draining the other slot's DMA too.  The waits are explicit

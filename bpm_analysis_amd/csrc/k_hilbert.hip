@@ -230,15 +230,9 @@ __device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &
         const double2 w1 = (INV && n2) ? S.tw(step * n2) : make_double2(1.0, 0.0);
         const double2 wp = (INV && n2) ? S.tw(step * n2 * p) : make_double2(1.0, 0.0);
         double2 tn = w1;
-        /* each step's two LDS reads are issued a step ahead */
-        double2 un = S.x[base + L], vn = S.x[base + (p - 1) * L];
 #pragma unroll 1
         for (int n = 1; n <= h; ++n, row += 2 * G) {
-            double2 u = un, v = vn;
-            if (n < h) {
-                un = S.x[base + (n + 1) * L];
-                vn = S.x[base + (p - n - 1) * L];
-            }
+            double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
             if (INV && n2) {
                 u = cmulc(u, tn);
                 v = cmulc(v, cmulc(wp, tn));
@@ -479,8 +473,15 @@ __device__ __forceinline__ void hb_rader197(const HbLds &S, const HilbPlan &P, c
                 e = (e * 33) % PR;
             }
             hb_dft14<false>(v);
+            /* W_196^(c k1) as powers of W_196^c (lanes' table indices c k1 are
+             * strided: the per-k1 reads were bank-conflicted) */
+            const double2 wc = W[c];
+            double2 tw = wc;
 #pragma unroll
-            for (int k1 = 1; k1 < R; ++k1) v[k1] = cmul(v[k1], W[c * k1]);
+            for (int k1 = 1; k1 < R; ++k1) {
+                v[k1] = cmul(v[k1], tw);
+                tw = cmul(tw, wc);
+            }
         }
         __syncthreads();
         if (act) {
@@ -496,8 +497,13 @@ __device__ __forceinline__ void hb_rader197(const HbLds &S, const HilbPlan &P, c
 #pragma unroll
             for (int k2 = 0; k2 < R; ++k2) v[k2] = cmul(v[k2], Bh[c + R * k2]);
             hb_dft14<true>(v);                               /* over k2 -> m2 */
+            const double2 wc = W[c];
+            double2 tw = wc;
 #pragma unroll
-            for (int m2 = 1; m2 < R; ++m2) v[m2] = cmulc(v[m2], W[c * m2]);
+            for (int m2 = 1; m2 < R; ++m2) {
+                v[m2] = cmulc(v[m2], tw);
+                tw = cmul(tw, wc);
+            }
         }
         __syncthreads();
         if (act) {

@@ -31,6 +31,8 @@ for s in "$@"; do
     write) step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o run -- python3 bench.py --steps 3 --warmup 1 $Q ;;
     kt) step ktime 900 python tools/ktime.py ${KT:-build_var/libbpmx_head.so bpm_analysis_amd/libbpmx.so} ;;
     hb) step hbench 120 ./tools/hbench ;;
+    ov) step overlap 120 ./tools/overlap_probe ;;
+    c5h) step bench_c5_head 900 env BPMX_LIB=build_var/libbpmx_head.so python bench.py --workload c5 --c5-files 64 --steps 5 --warmup 2 ;;
     rqb) step rqbench 120 ./tools/rqbench /tmp/floor_in.bin ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown $s"; exit 2 ;;
