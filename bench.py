@@ -57,6 +57,11 @@ def parse(argv=None):
     ap.add_argument("--host-beat-files", type=int, default=16,
                     help="files of the side measurement of the host beat stages (0: skip)")
     ap.add_argument("--options", type=int, default=0, help="bpmx_option bits (diagnostics; 0 = defaults)")
+    ap.add_argument("--tie-check", default="on", choices=["on", "off"],
+                    help="the timed step's decisive-tie check (off: diagnostic A/B of its cost only)")
+    ap.add_argument("--batch-pipeline", default="auto", choices=["auto", "on", "off"],
+                    help="timed steps through engine.BatchPipeline (batch k+1's envelope beside batch k's "
+                         "detection, two contexts and streams); auto: on in reference mode")
     ap.add_argument("--contexts", type=int, default=4,
                     help="side measurement: the batch split over K contexts on K streams (0: skip)")
     ap.add_argument("--exact-steps", type=int, default=5,
@@ -665,6 +670,8 @@ def main(args):
         for k in range(k_steps):
             o = outs_pp[k & 1]
             step(o)
+            if args.tie_check == "off":
+                continue
             h = det.tie_check_start(o)
             if pend is not None:
                 r = det.tie_check_finish(pend[0], pend[1], params, N.STAGE_ALL, args.options)
@@ -686,20 +693,55 @@ def main(args):
         dist.barrier()
     # timed steps: events around the dominant kernel's launches only, so the
     # step time carries no per-launch event overhead
-    det.profile_only(dom)
-    det.profile(True)
+    # Reference mode's envelope is a few waves of sequential passes, so a
+    # stream of batches runs batch k+1's envelope beside batch k's detection
+    # (engine.BatchPipeline, two contexts on two streams): a step is still one
+    # batch through every stage and its tie check, the K steps overlap.
+    piped = args.batch_pipeline == "on" or (args.batch_pipeline == "auto" and args.mode == "reference")
+    piped = piped and not args.cpu_stub
+    pipe = None
+    if piped:
+        from bpm_analysis_amd.engine import BatchPipeline
+        pipe = BatchPipeline(local, fo, fs, params, mode=args.mode, options=args.options, d=d)
+        for _ in range(2):
+            pipe.submit(pcm)
+        pipe.finish()
+        pipe.ties_resolved = 0
+        for x in (pipe.env_det, pipe.det_det):
+            x.profile_only(dom)
+            x.profile(True)
+    else:
+        det.profile_only(dom)
+        det.profile(True)
     sync(det)
     ties["raised"] = 0
     t0 = time.perf_counter()
-    last = run_steps(args.steps)
+    if piped:
+        for _ in range(args.steps):
+            last = pipe.submit(pcm)
+        pipe.finish()
+    else:
+        last = run_steps(args.steps)
     sync(det)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    det.profile(False)
-    prof = det.profile_read()
+    if piped:
+        prof = {}
+        for x in (pipe.env_det, pipe.det_det):
+            x.profile(False)
+            for k, (c, tms) in x.profile_read().items():
+                c0, t_0 = prof.get(k, (0, 0.0))
+                prof[k] = (c0 + c, t_0 + tms)
+        ties["raised"] = pipe.ties_resolved
+    else:
+        det.profile(False)
+        prof = det.profile_read()
     gpu_host = last.to_host()          # the timed steps' outputs (checked against the oracle below)
     ties_timed = dict(ties)
+    if pipe is not None:
+        pipe.close()
+        del pipe
     elapsed, total_peaks = reduce_results(t1 - t0, out.n_peaks, world, rank)
     # per-kernel table from a separate, untimed pass with every launch bracketed
     det.profile_only("")
@@ -1019,6 +1061,9 @@ def main(args):
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 5),
                     "traffic": pmc_traffic(args.mode, dom, workload, cnt / args.steps),
+                    "traffic_source": f"profiles/pmc_traffic_{args.mode}.json: rocprofv3 --pmc FETCH_SIZE / "
+                                      "WRITE_SIZE passes of this command (tools/pmc_traffic.py), committed; "
+                                      "read here, not measured in this run",
                     "kernel": dom, "kernel_ms_per_step": round(per_step_s * 1e3, 4),
                     "launches_per_step": cnt / args.steps, "algorithmic_bytes_per_step": abytes[dom]}
         kernels = {}
@@ -1051,7 +1096,8 @@ def main(args):
             "data": "cpu-stub (tests only; not a measurement)" if args.cpu_stub else "synthetic",
             "config": {"workload": workload, "files_total": total_files,
                        "files_per_gpu": F, "frames_per_file": n, "decimated_per_file": nd, "mode": args.mode,
-                       "parallelism": f"file-sharded x{world}"},
+                       "parallelism": f"file-sharded x{world}",
+                       "batch_pipeline": bool(piped)},
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "pipeline": pipeline, "pcie_inclusive": pcie, "kernels": kernels, "total_raw_peaks": total_peaks,

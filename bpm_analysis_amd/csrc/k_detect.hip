@@ -993,16 +993,25 @@ __global__ __launch_bounds__(FP_T, 8) void k_find_peaks_lds(PeakArgs A) {
         for (int gi = 0; gi <= M; ++gi) {
             for (int lr = 0; lr <= M; ++lr) {
                 bool progress = false;
+                /* the neighbour counts opaque per round: otherwise the 24
+                 * (r, q < nbc[r]) lane masks are hoisted out of the rounds into
+                 * SGPRs, which spill, and every round pays a readlane per mask */
+                int nbv[FP_R];
+#pragma unroll
+                for (int r = 0; r < FP_R; ++r) {
+                    nbv[r] = nbc[r];
+                    asm volatile("" : "+v"(nbv[r]));
+                }
                 /* every listed neighbour's state first (independent LDS reads),
                  * then the decisions */
                 uint32_t kill = 0u, block = 0u;
 #pragma unroll
                 for (int r = 0; r < FP_R; ++r) {
-                    if (!((und >> r) & 1u) || nbc[r] < 0) continue;
+                    if (!((und >> r) & 1u) || nbv[r] < 0) continue;
                     const int j = tid + r * FP_T;
 #pragma unroll
                     for (int q = 0; q < FP_NB; ++q) {
-                        if (q < nbc[r]) {
+                        if (q < nbv[r]) {
                             const int k = j + (int)(int8_t)((nb[r][q >> 2] >> (8 * (q & 3))) & 0xFFu);
                             const uint8_t st = ld_state(&s_st[k]);
                             kill |= (st == ST_KEPT ? 1u : 0u) << r;

@@ -678,7 +678,7 @@ __device__ __forceinline__ double db_walk(const DbSeg *sg, int m, int32_t lo, in
  * trough values): the recording then gets the full draft. */
 constexpr int DP_SPL_MAX = 4;
 #ifndef BPMX_DP_WAVES
-#define BPMX_DP_WAVES 6   /* waves per SIMD the one-segment k_draft_points is compiled for */
+#define BPMX_DP_WAVES 5   /* waves per SIMD the one-segment k_draft_points is compiled for (r06: 6 spilled 33 VGPRs; 5: 0.114 -> 0.106 ms on the reference sample) */
 #endif
 constexpr int DP_IP_ROUNDS = 8;
 constexpr int DP_FIX = 4;         /* exact steps after a segment's inverse estimate before bisection */   /* interpolated value pivots before random element pivots */

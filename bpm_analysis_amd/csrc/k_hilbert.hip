@@ -239,6 +239,10 @@ __device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &
                 tn = cmul(tn, w1);
             }
             const double2 a = cadd(u, v), b = csub(u, v);
+#ifdef HB_CP_NOFMA                                           /* tools/hbench timing diagnostic (wrong outputs) */
+            ax[0] += a.x + row[0]; ay[0] += a.y; bx[0] += b.x; by[0] += b.y;
+            if (false)
+#endif
 #pragma unroll
             for (int j = 0; j < G; ++j) {
                 const double c = row[j], sn = row[G + j];
@@ -267,6 +271,10 @@ __device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &
         tk = S.tw(step * n2 * g * G);
     }
     __syncthreads();
+#ifdef HB_CP_NOWRITE                                          /* tools/hbench timing diagnostic (wrong outputs) */
+    if (act && r0[0].x == 1.2345e300) S.x[base] = r1[G - 1];
+    if (false)
+#endif
     if (act) {
 #pragma unroll
         for (int j = 0; j < G; ++j) {

@@ -424,6 +424,128 @@ class Detector:
         return res
 
 
+class BatchPipeline:
+    """Batches of one geometry through the path back to back, batch k + 1's
+    ENVELOPE stage overlapping batch k's detection (FLOOR | PEAKS and the
+    decisive-tie check).
+
+    Reference mode's envelope is three bit-exact sequential passes (DF2T
+    forward and backward, pandas' Kahan rolling mean, bpm_analysis.py:1045-1054)
+    with one lane per recording: 1024 recordings are 16 waves, so for ~2.8 ms
+    per batch 240 of the 256 CUs idle, and the detection after it fills the
+    chip for ~1.3 ms.  Two library contexts on two HIP streams run the two
+    halves of consecutive batches at the same time (the streams' kernels do
+    overlap on MI355X: tools/overlap_probe), so a stream of batches costs
+    max(envelope, detection) per batch instead of their sum.  ``depth`` result
+    sets rotate; batch k's envelope waits (an event, no host wait) until the
+    detection that last used its result set is done.
+
+    ``submit(pcm)`` enqueues one batch and returns its Result (complete once
+    ``finish`` or a later ``submit`` has checked it); ``finish()`` drains.
+    Every batch's outputs equal a single ``Detector.run`` of all stages."""
+
+    def __init__(self, device: int, frame_offsets: Sequence[int], fs: int, params: dict, mode: str = "reference",
+                 channels: int = 1, options: int = 0, depth: int = 2, d: Optional[Design] = None,
+                 det_free_cus: int = 32, env_priority: bool = True, env_masked: bool = False):
+        torch = _torch()
+        self.fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
+        self.fs, self.params, self.mode, self.channels, self.options = fs, params, mode, channels, options
+        self.d = d if d is not None else design(fs, params, log=False)
+        self.env_det, self.det_det = Detector(device), Detector(device)
+        # The envelope chain is a sequence of small launches: each needs a free
+        # CU when it starts, and a detection kernel's workgroups hold a whole
+        # CU's LDS for ~0.1 ms each.  So the detection stream leaves
+        # `det_free_cus` CUs out of its mask (spread over the XCDs), and the
+        # envelope stream has the higher priority for the CUs that do free up.
+        if env_masked:
+            self.s_env = cu_masked_stream(self.env_det.device, det_free_cus, only=True)
+        else:
+            self.s_env = torch.cuda.Stream(self.env_det.device, priority=-1 if env_priority else 0)
+        self.s_det = cu_masked_stream(self.det_det.device, det_free_cus)
+        self.outs = [self.det_det.alloc(self.fo, self.d.ds, self.d.sr) for _ in range(max(2, depth))]
+        self.ev_free = [None] * len(self.outs)
+        self.pending = None
+        self.k = 0
+        self.ties_resolved = 0
+
+    def _check(self, pend):
+        """Batch `pend`'s tie check (its read-back was queued behind its
+        detection); a resolution runs on the detection stream and re-marks
+        when the batch's result set is free."""
+        if pend is None:
+            return
+        torch = _torch()
+        h, o, i = pend
+        with torch.cuda.stream(self.s_det):
+            r = self.det_det.tie_check_finish(h, o, self.params, N.STAGE_FLOOR | N.STAGE_PEAKS, self.options)
+            if r:
+                ev = torch.cuda.Event()
+                ev.record(self.s_det)
+                self.ev_free[i] = ev
+        self.ties_resolved += r
+
+    def submit(self, pcm) -> Result:
+        torch = _torch()
+        i = self.k % len(self.outs)
+        o = self.outs[i]
+        with torch.cuda.stream(self.s_env):
+            if self.ev_free[i] is not None:
+                self.s_env.wait_event(self.ev_free[i])
+            self.env_det.run(pcm, self.fo, self.fs, self.params, mode=self.mode, stages=N.STAGE_ENVELOPE,
+                             channels=self.channels, out=o, d=self.d, options=self.options)
+            ev_env = torch.cuda.Event()
+            ev_env.record(self.s_env)
+        with torch.cuda.stream(self.s_det):
+            self.s_det.wait_event(ev_env)
+            self.det_det.run(None, self.fo, self.fs, self.params, mode=self.mode,
+                             stages=N.STAGE_FLOOR | N.STAGE_PEAKS, channels=self.channels, out=o, d=self.d,
+                             options=self.options)
+            h = self.det_det.tie_check_start(o)
+            ev_free = torch.cuda.Event()
+            ev_free.record(self.s_det)
+            self.ev_free[i] = ev_free
+        # batch k - 1's tie check, with batch k's envelope and detection already queued
+        prev, self.pending = self.pending, (h, o, i)
+        self._check(prev)
+        self.k += 1
+        return o
+
+    def finish(self):
+        torch = _torch()
+        prev, self.pending = self.pending, None
+        self._check(prev)
+        self.s_env.synchronize()
+        self.s_det.synchronize()
+        torch.cuda.current_stream(self.det_det.device).wait_stream(self.s_det)
+
+    def close(self):
+        self.env_det.close()
+        self.det_det.close()
+
+
+def cu_masked_stream(device, free_cus: int, only: bool = False):
+    """A torch stream on `device` whose kernels avoid the first `free_cus` CUs
+    of the mask (or, with `only`, run on those alone).  hipExtStreamCreateWithCUMask:
+    bit c of the mask is the (c / 8)-th CU of XCD c % 8, so the first
+    `free_cus` bits are the same share of every XCD.  free_cus <= 0: an
+    ordinary stream."""
+    torch = _torch()
+    if free_cus <= 0:
+        return torch.cuda.Stream(device)
+    hip = ctypes.CDLL("libamdhip64.so")
+    total = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (total + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in (range(0, min(free_cus, total)) if only else range(min(free_cus, total), total)):
+        mask[c // 32] |= 1 << (c % 32)
+    st = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise N.BpmxError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(st.value, device=device)
+
+
 def _torch_np_map():
     torch = _torch()
     return {np.dtype(np.uint8): torch.uint8, np.dtype(np.int16): torch.int16, np.dtype(np.int32): torch.int32,

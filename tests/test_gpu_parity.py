@@ -480,6 +480,39 @@ def test_rollq_pruning_exact(det):
         assert _same(a["troughs"], ot)
 
 
+def test_long_quantiles_adversarial(det):
+    """Long recordings' quantiles (k_qv_*: key bins over the recording's own
+    range, the target bin's keys gathered, an exact select among them) on
+    envelopes that put many keys in one bin or spread them over the whole
+    double range: floor, troughs, raw peaks and flags equal to the oracle
+    (np.quantile, bit for bit), in one ragged batch with short recordings."""
+    from bpm_analysis_amd import _native as N
+    params = dict(G.BASE_PARAMS)
+    rng = np.random.default_rng(23)
+    m = 60_000
+    t = np.arange(m)
+    beat = np.maximum(0.0, np.sin(2 * np.pi * t / 250.0)) ** 8
+    envs = [
+        np.full(m, 7.0) + 300 * (t % 911 == 0),                              # one value nearly everywhere
+        np.geomspace(1e-300, 1e300, m)[rng.permutation(m)] + 0.0,              # every octave of the range
+        np.round(10.0 + 0.001 * t, 1) + 300 * beat,                            # long runs of equal values
+        np.where(t % 3 == 0, 0.0, 1e-12 * rng.random(m)) + 50 * beat,          # zeros and tiny values
+        rng.pareto(1.5, m) + 30 * beat,                                        # heavy tail
+        300 * beat[:20_000] + rng.random(20_000),                              # short: k_quantile_reg
+    ]
+    sr = 302
+    d = O.derive(sr, params)
+    got = det.run_env_host(envs, sr, params, N.STAGE_FLOOR | N.STAGE_PEAKS)
+    for env, r in zip(envs, got):
+        of, ot, ofl = O.noise_floor(env, d, params)
+        opk = O.raw_peaks(env, of, d, params)
+        assert _same(r["floor"], of)
+        assert _same(r["troughs"], ot)
+        assert _same(r["peaks"], opk)
+        mask = FALLBACK_BITS | 4 | O.F_TROUGH_TIE       # decisive-tie reports: the oracle's are exact too
+        assert (r["flags"] & mask) == (ofl & mask)
+
+
 def test_find_peaks_kernels_agree(det):
     """find_peaks with prominences from the LDS-resident local extrema
     (k_find_peaks_lds, default) equals the sample walks over global memory
@@ -1241,6 +1274,42 @@ def test_pipelined_run_identical(mode):
                     assert _same(a[k], b[k]), (shape, k)
         det.close()
     ref_det.close()
+
+
+@pytest.mark.parametrize("mode", ["reference", "native"])
+def test_batch_pipeline_identical(det, mode):
+    """engine.BatchPipeline (batch k + 1's envelope on one context and stream
+    beside batch k's detection on another) gives, for every batch of a
+    stream, the single all-stage run's outputs: env and floor bit for bit,
+    troughs, peaks and flags identical; four different ragged batches through
+    two result sets, so the result-set reuse and the cross-stream events are
+    exercised."""
+    from bpm_analysis_amd.engine import BatchPipeline
+    fs = 44100
+    lens = [fs * 20, fs * 7 + 13, fs * 31, fs * 12 + 5, fs * 16]
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    pcms = [det.synth(fo, fs, 1, seed0=900 + 10 * b) for b in range(4)]
+    want = []
+    for p in pcms:
+        r = det.run(p, fo, fs, params, mode=mode)
+        det.resolve_ties(r, params)
+        want.append(r.to_host())
+    pipe = BatchPipeline(0, fo, fs, params, mode=mode)
+    got = []
+    for b, p in enumerate(pcms):
+        got.append(pipe.submit(p))
+        if b % 2 == 1:                   # read back before the set is reused
+            pipe.finish()
+            got = got[:-2] + [x.to_host() for x in got[-2:]]
+    pipe.finish()
+    pipe.close()
+    assert len(got) == 4
+    for g, w in zip(got, want):
+        for a, b in zip(g, w):
+            assert a["flags"] == b["flags"]
+            for k in ("env", "floor", "troughs", "peaks"):
+                assert _same(a[k], b[k]), k
 
 
 def test_native_envelope_independent_of_placement(det):

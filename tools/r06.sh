@@ -22,6 +22,8 @@ for s in "$@"; do
     pt) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 600 python bench.py $Q ;;
+    benchq_notie) step benchq_notie 600 python bench.py $Q --tie-check off ;;
+    benchq_pipe) step benchq_pipe 600 python bench.py $Q --batch-pipeline on ;;
     bench_ref) step bench_ref 600 python bench.py --mode reference --steps 10 --warmup 2 --real-env-steps 0 ;;
     c5) step bench_c5_64 900 python bench.py --workload c5 --c5-files 64 --steps 5 --warmup 2 ;;
     stats) step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_stats -o run -- python3 bench.py --steps 5 --warmup 1 $Q ;;
@@ -32,6 +34,9 @@ for s in "$@"; do
     kt) step ktime 900 python tools/ktime.py ${KT:-build_var/libbpmx_head.so bpm_analysis_amd/libbpmx.so} ;;
     hb) step hbench 120 ./tools/hbench ;;
     ov) step overlap 120 ./tools/overlap_probe ;;
+    rep) step realenv 900 python tools/realenv_prof.py reference ${REP:-build_var/libbpmx_head.so bpm_analysis_amd/libbpmx.so} ;;
+    rpp) step refpipe 800 python tools/refpipe_probe.py reference ;;
+    bench_ref_off) step bench_ref_off 600 python bench.py --mode reference --steps 10 --warmup 2 --real-env-steps 0 --batch-pipeline off --no-cpu --contexts 0 --pcie-steps 0 --exact-steps 0 --host-beat-files 0 --dropin-files 0 ;;
     c5h) step bench_c5_head 900 env BPMX_LIB=build_var/libbpmx_head.so python bench.py --workload c5 --c5-files 64 --steps 5 --warmup 2 ;;
     rqb) step rqbench 120 ./tools/rqbench /tmp/floor_in.bin ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
