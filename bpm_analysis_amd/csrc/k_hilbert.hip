@@ -201,6 +201,9 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, const HilbPlan &P, int
  * registers for the barrier, then go back in place (with the DIF's
  * twiddles).  One round of waves: the plan takes this form only when
  * ng ceil((M / p) / 64) <= HB_T / 64. */
+#ifndef HB_CP_UNROLL
+#define HB_CP_UNROLL 1
+#endif
 __host__ __device__ constexpr int hb_cp_ng(int p) { return ((p + 1) / 2 + HB_CP_G - 1) / HB_CP_G; }
 
 template <bool INV>
@@ -230,7 +233,7 @@ __device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &
         const double2 w1 = (INV && n2) ? S.tw(step * n2) : make_double2(1.0, 0.0);
         const double2 wp = (INV && n2) ? S.tw(step * n2 * p) : make_double2(1.0, 0.0);
         double2 tn = w1;
-#pragma unroll 1
+#pragma unroll HB_CP_UNROLL
         for (int n = 1; n <= h; ++n, row += 2 * G) {
             double2 u = S.x[base + n * L], v = S.x[base + (p - n) * L];
             if (INV && n2) {
@@ -245,7 +248,11 @@ __device__ __forceinline__ void hb_radixp_const(const HbLds &S, const HilbPlan &
 #endif
 #pragma unroll
             for (int j = 0; j < G; ++j) {
+#ifdef HB_CP_NOROW                                            /* tools/hbench timing diagnostic (wrong outputs) */
+                const double c = 0.5 + j, sn = 0.25 - j;
+#else
                 const double c = row[j], sn = row[G + j];
+#endif
                 ax[j] = __builtin_fma(a.x, c, ax[j]);
                 ay[j] = __builtin_fma(a.y, c, ay[j]);
                 bx[j] = __builtin_fma(b.x, sn, bx[j]);

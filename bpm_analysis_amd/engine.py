@@ -446,7 +446,7 @@ class BatchPipeline:
 
     def __init__(self, device: int, frame_offsets: Sequence[int], fs: int, params: dict, mode: str = "reference",
                  channels: int = 1, options: int = 0, depth: int = 2, d: Optional[Design] = None,
-                 det_free_cus: int = 32, env_priority: bool = True, env_masked: bool = False):
+                 det_free_cus: int = 48, env_priority: bool = True, env_masked: bool = False):
         torch = _torch()
         self.fo = np.ascontiguousarray(frame_offsets, dtype=np.int64)
         self.fs, self.params, self.mode, self.channels, self.options = fs, params, mode, channels, options

@@ -31,9 +31,8 @@ for _ in range(steps):
 torch.cuda.synchronize()
 print(f"{mode} unpipelined: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/batch", flush=True)
 ref = out.to_host()
-configs = [(16, True, False), (32, True, False), (64, True, False), (96, True, False), (128, True, False),
-           (16, False, True), (32, False, True), (64, False, True)]
-for free, prio, emask in configs * 2:
+configs = [(16, True, False), (32, True, False), (48, True, False), (64, True, False), (128, True, False)]
+for free, prio, emask in configs * 3:
     p = BatchPipeline(0, fo, fs, params, mode=mode, d=d, det_free_cus=free, env_priority=prio, env_masked=emask)
     for _ in range(2):
         p.submit(pcm)
