@@ -764,11 +764,13 @@ __global__ __launch_bounds__(64 * NW, 1) void k_native_blocks_mfma_big(NatBlockA
      * last whole chunk */
     auto dma = [&](int64_t e0, u4 *slot) {
         const int64_t a0 = e0 & ~(int64_t)7;
+        int nchv = nch, lanev = lane;                     /* opaque: no hoisted lane masks (k_native_blocks_mfma) */
+        asm volatile("" : "+s"(nchv), "+v"(lanev));
 #pragma unroll
         for (int r = 0; r < NDMA; ++r) {
-            const int q = r * 64 + lane;
+            const int q = r * 64 + lanev;
             int64_t c = a0 + (int64_t)q * 8;
-            c = (q < nch && c + 8 <= total) ? c : clast;
+            c = (q < nchv && c + 8 <= total) ? c : clast;
             const uint32_t m0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)(slot + r * 64);
             asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                          :: "v"(pcm + c), "s"(m0) : "memory");

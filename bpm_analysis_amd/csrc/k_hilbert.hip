@@ -202,7 +202,7 @@ __device__ __forceinline__ void hb_radixp(const HbLds &S, const HilbPlan &P, int
  * twiddles).  One round of waves: the plan takes this form only when
  * ng ceil((M / p) / 64) <= HB_T / 64. */
 #ifndef HB_CP_UNROLL
-#define HB_CP_UNROLL 1
+#define HB_CP_UNROLL 2   /* (r06 tools/hbench: 1 -> 2 made the radix-23 stage 20.2 K -> 19.7 K cycles) */
 #endif
 __host__ __device__ constexpr int hb_cp_ng(int p) { return ((p + 1) / 2 + HB_CP_G - 1) / HB_CP_G; }
 
