@@ -243,7 +243,20 @@ __global__ __launch_bounds__(256) void k_qv_hist(QvArgs A) {
     const QvRange g = A.rg[f];
     __syncthreads();
     const double *x = A.Q.env + d0;
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) atomicAdd(&hist[qv_bin(f64_key(x[i]), g)], 1u);
+    /* a wave's 64 consecutive samples fall in runs of equal bins (the
+     * envelope is smooth): one LDS atomic per run, with the run's length */
+    const int lane = lane_id();
+    for (int64_t i0 = c0 + (threadIdx.x & ~63); i0 < c1; i0 += 256) {   /* uniform per wave */
+        const int64_t i = i0 + lane;
+        const int nv = (int)min<int64_t>(64, c1 - i0);
+        const int b = i < c1 ? qv_bin(f64_key(x[i]), g) : -1;
+        const int bprev = __shfl_up(b, 1);
+        const bool start = b >= 0 && (lane == 0 || bprev != b);
+        const uint64_t sm = __ballot(start);
+        const uint64_t after = sm & ~((2ull << lane) - 1ull);
+        const int nxt = after ? __ffsll((long long)after) - 1 : nv;
+        if (start) atomicAdd(&hist[b], (unsigned int)(nxt - lane));
+    }
     __syncthreads();
     unsigned int *gh = A.hist + (int64_t)f * QV_BINS;
     for (int i = threadIdx.x; i < QV_BINS; i += 256) {

@@ -398,13 +398,19 @@ __global__ __launch_bounds__(FPC_T) void k_fpl_dist_ch(PeakArgs A, FplArgs L) {
         for (int lr = 0; lr <= m; ++lr) {
             bool progress = false;
             uint32_t kill = 0u, block = 0u;
+            int nbv[FPC_R];                                  /* opaque per round: no hoisted (r, q) masks (k_find_peaks_lds) */
 #pragma unroll
             for (int r = 0; r < FPC_R; ++r) {
-                if (!((und >> r) & 1u) || nbc[r] < 0) continue;
+                nbv[r] = nbc[r];
+                asm volatile("" : "+v"(nbv[r]));
+            }
+#pragma unroll
+            for (int r = 0; r < FPC_R; ++r) {
+                if (!((und >> r) & 1u) || nbv[r] < 0) continue;
                 const int j = tid + r * FPC_T;
 #pragma unroll
                 for (int q = 0; q < NBX; ++q) {
-                    if (q < nbc[r]) {
+                    if (q < nbv[r]) {
                         const int k = j + (int)(int8_t)((nb[r][q >> 2] >> (8 * (q & 3))) & 0xFFu);
                         const uint8_t sk = ld_state(&s_st[k]);
                         kill |= (sk == ST_KEPT ? 1u : 0u) << r;

@@ -258,36 +258,9 @@ __device__ __forceinline__ bool rollq_wm_body(RollqArgs A, uint16_t *pos_scratch
         uint8_t *bin8 = (uint8_t *)(hsc + NWV * NB);        /* [mall] bin of each sample */
         /* one 64-sample block per wave step: runs of equal bins (the curve is
          * piecewise monotone, so a block has few) each add their length */
-        /* the curve at 64 consecutive positions: the segment of each lane from
-         * the troughs inside the block (a uniform walk over their few
-         * positions), then its independent reads; dval's arithmetic */
-        auto dval_blk = [&](int x0, int xi) -> double {
-            if (!fused) return dval(xi);
-            if (ntr == 0 || xi < s_tp[0]) return __builtin_nan("");
-            int j = __builtin_amdgcn_readfirstlane(s_bj[(x0 - (int)xb) >> 6]);
-            j = j < 0 ? 0 : j;
-            while (j + 1 < ntr && __builtin_amdgcn_readfirstlane(s_tp[j + 1]) <= x0) ++j;   /* uniform */
-            int jl = j;
-            for (int qq = j + 1; qq < ntr; ++qq) {                                             /* uniform */
-                const int tq = __builtin_amdgcn_readfirstlane(s_tp[qq]);
-                if (tq > x0 + 63) break;
-                jl += tq <= xi ? 1 : 0;
-            }
-            const int tj = s_tp[jl];
-            const double vj = s_tv[jl];
-            if (jl == ntr - 1 || tj == xi) return vj;
-            const double y1 = s_tv[jl + 1];
-            const double slope = s_sl[jl];
-            double r = slope * ((double)xi - (double)tj) + vj;
-            if (r != r) {
-                r = slope * ((double)xi - (double)s_tp[jl + 1]) + y1;
-                if (r != r && vj == y1) r = vj;
-            }
-            return r;
-        };
         for (int p0 = wid << 6; p0 < mall; p0 += WM_T) {
             const int p = p0 + lane, nv = min(64, mall - p0);
-            const int b = p < mall ? vbin(dval_blk((int)t0 + p0, (int)t0 + p)) : -1;
+            const int b = p < mall ? vbin(dval(t0 + p)) : -1;
             if (p < mall) bin8[p] = (uint8_t)b;
             const int bprev = wave_shr1_dpp(b, -1);          /* all lanes active here */
             const bool start = b >= 0 && (lane == 0 || bprev != b);
