@@ -350,16 +350,14 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
             for (int i = tid; i < nr * n; i += LF_T) row0[i] = x[i];
             return;
         }
-        /* element k of row q times w_M^(q k): the thread's first from the
-         * table, the next ones by products with w_M^(q LF_T) (a few per
-         * thread; each table lookup was two scattered global loads) */
+        /* element k of row q times w_M^(q k): t = q k mod M stepped by q LF_T */
         for (int qq = 0; qq < nr; ++qq) {
-            const int64_t q = q0 + qq;
-            double2 w = twid(A.tab, rc, (q * tid) % M, sign);
-            const double2 wd = twid(A.tab, rc, (q * LF_T) % M, sign);
+            const int64_t q = q0 + qq, d = (q * LF_T) % M;
+            int64_t t = (q * tid) % M;
             for (int k = tid; k < n; k += LF_T) {
-                row0[(int64_t)qq * n + k] = cmul(x[qq * n + k], w);
-                w = cmul(w, wd);
+                row0[(int64_t)qq * n + k] = cmul(x[qq * n + k], twid(A.tab, rc, t, sign));
+                t += d;
+                if (t >= M) t -= M;
             }
         }
         return;
@@ -407,12 +405,12 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
             return;
         }
         for (int qq = 0; qq < nr; ++qq) {
-            const int64_t q = q0 + qq;
-            double2 w = twid(A.tab, rc, (q * tid) % M, sign);
-            const double2 wd = twid(A.tab, rc, (q * LF_T) % M, sign);
+            const int64_t q = q0 + qq, d = (q * LF_T) % M;
+            int64_t t = (q * tid) % M;
             for (int k = tid; k < n; k += LF_T) {
-                row0[(int64_t)qq * n + k] = cmul(xin[qq * n + k], w);
-                w = cmul(w, wd);
+                row0[(int64_t)qq * n + k] = cmul(xin[qq * n + k], twid(A.tab, rc, t, sign));
+                t += d;
+                if (t >= M) t -= M;
             }
         }
         return;
@@ -440,18 +438,14 @@ __global__ __launch_bounds__(LF_T) void k_lf_rows(LfArgs A, double2 *__restrict_
     __syncthreads();
     lds_fft(x, rt, L, 1, sbp->rad, nrad);
     const double invL = 1.0 / (double)L;
-    double2 w = make_double2(1.0, 0.0), wd = w;
-    if (tw) {
-        w = twid(A.tab, rc, ((int64_t)q0 * tid) % M, sign);
-        wd = twid(A.tab, rc, ((int64_t)q0 * LF_T) % M, sign);
-    }
+    const int64_t d = ((int64_t)q0 * LF_T) % M;
+    int64_t t = ((int64_t)q0 * tid) % M;
     for (int i = tid; i < n; i += LF_T) {
         double2 v = scale2(cmul(x[i], chirp(i)), invL);
-        if (tw) {
-            v = cmul(v, w);
-            w = cmul(w, wd);
-        }
+        if (tw) v = cmul(v, twid(A.tab, rc, t, sign));
         row0[i] = v;
+        t += d;
+        if (t >= M) t -= M;
     }
 }
 
