@@ -462,6 +462,7 @@ class BatchPipeline:
         else:
             self.s_env = torch.cuda.Stream(self.env_det.device, priority=-1 if env_priority else 0)
         self.s_det = cu_masked_stream(self.det_det.device, det_free_cus)
+        self._own = [s for s in (self.s_env, self.s_det) if isinstance(s, torch.cuda.ExternalStream)]
         self.outs = [self.det_det.alloc(self.fo, self.d.ds, self.d.sr) for _ in range(max(2, depth))]
         self.ev_free = [None] * len(self.outs)
         self.pending = None
@@ -519,8 +520,27 @@ class BatchPipeline:
         torch.cuda.current_stream(self.det_det.device).wait_stream(self.s_det)
 
     def close(self):
+        """Drain, free both contexts and destroy the CU-masked stream(s): a
+        stream left to the HIP runtime's exit-time teardown can outlive the
+        tools that hooked it (rocprofv3 faulted there)."""
+        if self.env_det is None:
+            return
+        self.s_env.synchronize()
+        self.s_det.synchronize()
         self.env_det.close()
         self.det_det.close()
+        for s in self._own:
+            destroy_stream(s)
+        self._own, self.env_det, self.det_det = [], None, None
+
+
+def destroy_stream(s):
+    """hipStreamDestroy of a stream cu_masked_stream made (torch does not own
+    an ExternalStream's handle)."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipStreamDestroy(ctypes.c_void_p(s.cuda_stream))
+    if rc != 0:
+        raise N.BpmxError(f"hipStreamDestroy failed ({rc})")
 
 
 def cu_masked_stream(device, free_cus: int, only: bool = False):
