@@ -19,34 +19,103 @@
 
 namespace bpmx {
 
-/* workgroup scratch (LDS) of the select; ~3.7 KB */
-struct QrShared {
-    unsigned int hist[256];
+#ifdef BPMX_QS_STAMPS                  /* tools/hbench -DBPMX_QS_STAMPS: per-phase cycles of the select */
+__device__ unsigned long long qs_dbg[8 * 4096];
+#define QS_DECL unsigned long long qs_acc[8] = {0}, qs_t = __builtin_amdgcn_s_memtime();
+#define QS_T(k)                                                                   \
+    do {                                                                          \
+        if (threadIdx.x == 0) {                                                   \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();           \
+            qs_acc[k] += t_ - qs_t;                                               \
+            qs_t = t_;                                                            \
+        }                                                                         \
+    } while (0)
+#define QS_FLUSH()                                                                \
+    do {                                                                          \
+        if (threadIdx.x == 0)                                                     \
+            for (int k_ = 0; k_ < 8; ++k_) qs_dbg[(blockIdx.x & 4095) * 8 + k_] = qs_acc[k_]; \
+    } while (0)
+#else
+#define QS_DECL
+#define QS_T(k) do {} while (0)
+#define QS_FLUSH() do {} while (0)
+#endif
+
+/* workgroup scratch (LDS) of the select; ~18 KB */
+struct alignas(16) QrShared {
+    unsigned int hw[QR_T / 64][256];   /* per-wave digit histograms (no cross-wave atomics on one bin) */
     unsigned int hist0[256];       /* the first varying digit's histogram: the same for every level */
     long long r;
-    int digit, csel, cc;
+    int digit, csel, cc, nxt;
     unsigned long long ck[64];
+    unsigned long long va, vb;
     unsigned long long a[QR_T / 64], b[QR_T / 64];
     long long cnt[QR_T / 64];
 };
 
+/* adds the wave's digits (dg < 0: none) to its own histogram row h with one
+ * LDS atomic per run of equal digits over consecutive lanes (item it of the 64
+ * lanes is 64 consecutive positions of a smooth envelope: a few runs).  A
+ * uniform-digit fast path (one atomic of the ballot's count) measured slower.
+ * Every lane must be active. */
+__device__ __forceinline__ void qr_hist_add(unsigned int *h, int dg) {
+    const int lane = lane_id();
+    const int prev = wave_shr1_dpp(dg, -2);                  /* lane 0: -2, never a digit or -1 */
+    const uint64_t bm = __ballot(prev != dg);                /* run starts */
+    const uint64_t after = bm & ~((2ull << lane) - 1ull);
+    const int nxt = after ? __ffsll((long long)after) - 1 : 64;
+    if (dg >= 0 && ((bm >> lane) & 1ull)) atomicAdd(&h[dg], (unsigned int)(nxt - lane));
+}
+
+/* wave-wide OR / AND / unsigned min of a 64-bit value by DPP row shifts and
+ * broadcasts (no LDS round trips), the result uniform.  Every lane active. */
+template <int OP>   /* 0 OR, 1 AND, 2 MIN */
+__device__ __forceinline__ uint64_t qr_wave_red64(uint64_t x) {
+    const uint64_t id = OP == 0 ? 0ull : ~0ull;
+    const int idl = (int)(uint32_t)id, idh = (int)(uint32_t)(id >> 32);
+#define QR_DPP_STEP(ctrl, rmask)                                                                  \
+    {                                                                                             \
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(idl, (int)(uint32_t)x, ctrl, rmask, 0xf, false); \
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(idh, (int)(uint32_t)(x >> 32), ctrl, rmask, 0xf, false); \
+        const uint64_t t = ((uint64_t)hi << 32) | lo;                                             \
+        x = OP == 0 ? (x | t) : OP == 1 ? (x & t) : (t < x ? t : x);                              \
+    }
+    QR_DPP_STEP(0x111, 0xf)   /* row_shr:1 */
+    QR_DPP_STEP(0x112, 0xf)   /* row_shr:2 */
+    QR_DPP_STEP(0x114, 0xf)   /* row_shr:4 */
+    QR_DPP_STEP(0x118, 0xf)   /* row_shr:8 */
+    QR_DPP_STEP(0x142, 0xa)   /* row_bcast:15 -> rows 1, 3 */
+    QR_DPP_STEP(0x143, 0xc)   /* row_bcast:31 -> rows 2, 3 */
+#undef QR_DPP_STEP
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 /* every thread of the QR_T-thread workgroup calls this with its QR_IT keys
- * (positions >= n ignored); writes A.qv[f][slot] for every level */
+ * (positions >= n ignored); writes A.qv[f][slot] for every level.
+ * Per digit pass: each wave counts into its own histogram row (run-length
+ * atomics), one barrier, wave 0 sums the rows, scans and picks the digit, one
+ * barrier.  The (r+1)-th smallest comes from the gathered keys when it lies
+ * under the same prefix (a final pass over all keys only when it does not).
+ * (r05 form: one shared histogram, atomics per item, ds_bpermute reductions:
+ * 45 K cycles per recording, most of it same-bin atomics from all waves and
+ * LDS round trips of the reductions, tools/hbench HB_Q=1.) */
 __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t n, const QuantArgs &A, int f,
                                           QrShared &S) {
     const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
     constexpr int NW = QR_T / 64;
+    QS_DECL
     uint64_t kor = 0, kand = ~0ull;
 #pragma unroll
     for (int it = 0; it < QR_IT; ++it) {
         const int64_t i = (int64_t)it * QR_T + tid;
         if (i < n) { kor |= key[it]; kand &= key[it]; }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        kor |= (uint64_t)__shfl_xor((long long)kor, o);
-        kand &= (uint64_t)__shfl_xor((long long)kand, o);
-    }
+    kor = qr_wave_red64<0>(kor);
+    kand = qr_wave_red64<1>(kand);
     if (lane == 0) { S.a[wid] = kor; S.b[wid] = kand; }
+    unsigned int *hrow = S.hw[wid];
     __syncthreads();
     uint64_t vary, common;
     {
@@ -55,58 +124,76 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
         vary = o ^ a;
         common = a;                                          /* the bits every key shares */
     }
-    __syncthreads();
+    QS_T(0);
+#if defined(QS_STOP) && QS_STOP == 1                             /* timing diagnostics (wrong outputs) */
+    return;
+#endif
     /* every level's first pass has no prefix yet: one histogram of the
      * highest varying digit serves them all */
     int shift0 = -1;
     for (int sh = 56; sh >= 0; sh -= 8)
         if ((vary >> sh) & 0xFFull) { shift0 = sh; break; }
-    if (shift0 >= 0) {
-        if (tid < 256) S.hist0[tid] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < QR_IT; ++it) {
-            const int64_t i = (int64_t)it * QR_T + tid;
-            if (i < n) atomicAdd(&S.hist0[(key[it] >> shift0) & 255], 1u);
-        }
-        __syncthreads();
-    }
+    /* items with a position < n: this thread's count, and the wave-uniform
+     * bound; copied opaquely into each item loop below, or the compiler hoists
+     * the 24 per-item lane masks out of the level and digit loops into SGPRs
+     * that spill */
+    const int nvt = n > tid ? (int)((n - tid + QR_T - 1) / QR_T) : 0;
+    const int nvu = __builtin_amdgcn_readfirstlane((int)((n + QR_T - 1) / QR_T));
     for (int l = 0; l < A.n_levels; ++l) {
         const double q = A.q[l];
         const double vi = (double)(n - 1) * q;
         const bool top = vi >= (double)(n - 1);
         const long long lo = top ? (long long)(n - 1) : (long long)floor(vi);
         uint64_t prefix = 0, mask = 0;
-        long long r = lo;
+        long long r = lo, binsz = n;                         /* rank within the keys under the prefix, their count */
+        bool gathered = false, have_b = top;
+        uint64_t kb = 0;
         for (int shift = 56; shift >= 0; shift -= 8) {
             if (((vary >> shift) & 0xFFull) == 0) {          /* uniform: constant digit */
                 prefix |= common & (0xFFull << shift);
                 mask |= 0xFFull << shift;
                 continue;
             }
-            const unsigned int *hs = shift == shift0 ? S.hist0 : S.hist;   /* uniform */
-            if (shift != shift0) {
-                if (tid < 256) S.hist[tid] = 0;
-                __syncthreads();
+            const bool first = shift == shift0;              /* uniform */
+            if (!(first && l > 0)) {                         /* level 0's first pass made hist0 */
+                reinterpret_cast<uint4 *>(hrow)[lane] = make_uint4(0u, 0u, 0u, 0u);   /* own row: no barrier */
+                int nv = nvt, nu = nvu;
+                asm volatile("" : "+v"(nv), "+s"(nu));
+                /* on 32-bit halves: the prefix test as two masked compares,
+                 * the digit as one bit-field extract */
+                auto rfl = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };   /* uniform values */
+                uint32_t mh = rfl((uint32_t)(mask >> 32)), ml = rfl((uint32_t)mask);
+                uint32_t ph = rfl((uint32_t)(prefix >> 32)), pl = rfl((uint32_t)prefix);
+                uint32_t dsh = rfl((uint32_t)(shift & 31)), dhi = rfl(shift >= 32 ? 1u : 0u);
+                asm volatile("" : "+s"(mh), "+s"(ml), "+s"(ph), "+s"(pl), "+s"(dsh), "+s"(dhi));
 #pragma unroll
-                for (int it = 0; it < QR_IT; ++it) {
-                    const int64_t i = (int64_t)it * QR_T + tid;
-                    if (i < n && (key[it] & mask) == prefix) atomicAdd(&S.hist[(key[it] >> shift) & 255], 1u);
-                }
+                for (int it = 0; it < QR_IT; ++it)
+                    if (it < nu) {                           /* uniform */
+                        const uint32_t kh = (uint32_t)(key[it] >> 32), kl = (uint32_t)key[it];
+                        const bool ok = it < nv && (kh & mh) == ph && (kl & ml) == pl;
+                        const int dg = (int)__builtin_amdgcn_ubfe(dhi ? kh : kl, dsh, 8u);
+                        qr_hist_add(hrow, ok ? dg : -1);
+                    }
                 __syncthreads();
             }
+            QS_T(2);
             if (wid == 0) {
-                const unsigned int c0 = hs[lane * 4], c1 = hs[lane * 4 + 1], c2 = hs[lane * 4 + 2], c3 = hs[lane * 4 + 3];
-                const long long sm = (long long)c0 + c1 + c2 + c3;
-                long long incl = sm;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const long long t = __shfl_up(incl, o);
-                    if (lane >= o) incl += t;
+                uint4 c4 = make_uint4(0u, 0u, 0u, 0u);
+                if (first && l > 0) {
+                    c4 = reinterpret_cast<const uint4 *>(S.hist0)[lane];
+                } else {
+#pragma unroll 4
+                    for (int w = 0; w < NW; ++w) {                   /* (a full unroll keeps 16 uint4 live beside the keys) */
+                        const uint4 h = reinterpret_cast<const uint4 *>(S.hw[w])[lane];
+                        c4.x += h.x; c4.y += h.y; c4.z += h.z; c4.w += h.w;
+                    }
+                    if (first) reinterpret_cast<uint4 *>(S.hist0)[lane] = c4;
                 }
-                const long long excl = incl - sm;
+                const int sm = (int)(c4.x + c4.y + c4.z + c4.w);   /* <= QR_MAX */
+                const int incl = wave_iscan_dpp<false>(sm), excl = incl - sm;
                 if (excl <= r && r < incl) {
                     long long rr = r - excl;
-                    const unsigned int cs[4] = {c0, c1, c2, c3};
+                    const unsigned int cs[4] = {c4.x, c4.y, c4.z, c4.w};
                     int d = 0;
                     while (rr >= (long long)cs[d]) { rr -= cs[d]; ++d; }
                     S.digit = lane * 4 + d;
@@ -116,18 +203,23 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
                 if (lane == 0) S.cc = 0;
             }
             __syncthreads();
+            QS_T(3);
+#if defined(QS_STOP) && QS_STOP == 2
+            return;
+#endif
             prefix |= (uint64_t)S.digit << shift;
             mask |= 0xFFull << shift;
             r = S.r;
-            if (shift > 0 && S.csel <= 64) {
+            binsz = S.csel;
+            if (shift > 0 && binsz <= 64) {
                 /* few keys left under the prefix (after one or two digits on
-                 * an envelope): gather them and take the r-th smallest directly
-                 * instead of the remaining digit passes */
+                 * an envelope): gather them and take the r-th and (r+1)-th
+                 * smallest directly instead of the remaining digit passes */
+                int nv = nvt;
+                asm volatile("" : "+v"(nv));
 #pragma unroll
-                for (int it = 0; it < QR_IT; ++it) {
-                    const int64_t i = (int64_t)it * QR_T + tid;
-                    if (i < n && (key[it] & mask) == prefix) S.ck[atomicAdd(&S.cc, 1)] = key[it];
-                }
+                for (int it = 0; it < QR_IT; ++it)
+                    if (it < nv && (key[it] & mask) == prefix) S.ck[atomicAdd(&S.cc, 1)] = key[it];
                 __syncthreads();
                 if (wid == 0) {
                     const int c = S.cc;
@@ -138,45 +230,49 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
                         below += o < mine;
                         same += o == mine;
                     }
-                    if (lane < c && below <= r && r < below + same) S.ck[0] = mine;   /* all writers agree */
+                    if (lane < c && below <= r && r < below + same) S.va = mine;        /* all writers agree */
+                    if (lane < c && below <= r + 1 && r + 1 < below + same) S.vb = mine;
                 }
                 __syncthreads();
-                prefix = S.ck[0];
+#if defined(QS_STOP) && QS_STOP == 3
+                return;
+#endif
+                prefix = S.va;
                 mask = ~0ull;
-                __syncthreads();
+                gathered = true;
+                if (!top && r + 1 < binsz) { kb = S.vb; have_b = true; }
+                QS_T(4);
                 break;
             }
+        }
+        if (!gathered && !top && r + 1 < binsz) {           /* every key under the full prefix is this one */
+            kb = prefix;
+            have_b = true;
         }
         const double va = key_f64(prefix);
         double res = va;
         if (!top) {
-            unsigned long long mn = ~0ull;
-            long long cnt = 0;
+            if (!have_b) {                                   /* the (r+1)-th is the smallest key above the prefix */
+                unsigned long long mn = ~0ull;
+                int nv = nvt;
+                asm volatile("" : "+v"(nv));
 #pragma unroll
-            for (int it = 0; it < QR_IT; ++it) {
-                const int64_t i = (int64_t)it * QR_T + tid;
-                if (i < n) {
-                    if (key[it] <= prefix) cnt++;
-                    else if (key[it] < mn) mn = key[it];
-                }
+                for (int it = 0; it < QR_IT; ++it)
+                    if (it < nv && key[it] > prefix && key[it] < mn) mn = key[it];
+                mn = qr_wave_red64<2>(mn);
+                if (lane == 0) S.a[wid] = mn;
+                __syncthreads();
+                unsigned long long m = S.a[0];
+                for (int w = 1; w < NW; ++w) m = S.a[w] < m ? S.a[w] : m;
+                kb = m;
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long om = __shfl_xor(mn, o);
-                mn = om < mn ? om : mn;
-                cnt += __shfl_xor(cnt, o);
-            }
-            __syncthreads();
-            if (lane == 0) { S.a[wid] = mn; S.cnt[wid] = cnt; }
-            __syncthreads();
-            unsigned long long m = S.a[0];
-            long long c = 0;
-            for (int w = 0; w < NW; ++w) { m = S.a[w] < m ? S.a[w] : m; c += S.cnt[w]; }
-            const double vb = (c > lo + 1) ? va : key_f64(m);
-            res = np_lerp(va, vb, vi - (double)lo);
+            res = np_lerp(va, key_f64(kb), vi - (double)lo);
         }
         if (tid < Q_SLOTS && ((A.slot[l] >> tid) & 1)) A.qv[(int64_t)f * Q_SLOTS + tid] = res;
         __syncthreads();
+        QS_T(5);
     }
+    QS_FLUSH();
 }
 
 }  // namespace bpmx

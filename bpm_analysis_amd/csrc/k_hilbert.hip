@@ -714,18 +714,30 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         if (i0 + j < i1) stage[i0 + j] = ev[j];
     __syncthreads();
     STAMP(10);
-    for (int i = threadIdx.x; i < N; i += HB_T) env[i] = stage[i];
+#ifdef HB_DIAG_NOQ                                              /* timing diagnostic: no select (wrong outputs) */
+    if (false) {
+#else
     if (A.q.n_levels > 0 && N <= QR_MAX) {
-        /* the detection stage's quantiles from the staged envelope (the same
-         * doubles just stored), so k_quantile_reg need not reload it */
+#endif
+        /* the detection stage's quantiles from the staged envelope, so
+         * k_quantile_reg need not reload it; each value read once for its
+         * global store and its key.  (The stores after the select instead,
+         * from the keys, made the kernel slower: 0.34 -> 0.356 ms; issued
+         * first they drain during the select.) */
         uint64_t key[QR_IT];
 #pragma unroll
         for (int it = 0; it < QR_IT; ++it) {
             const int i = it * HB_T + (int)threadIdx.x;
-            key[it] = i < N ? f64_key(stage[i]) : 0ull;
+            const double v = i < N ? stage[i] : 0.0;
+            if (i < N) env[i] = v;
+            key[it] = i < N ? f64_key(v) : 0ull;
         }
+        STAMP(11);
         __syncthreads();                                    /* the stage becomes the select's scratch */
         qr_select(key, N, A.q, f, *reinterpret_cast<QrShared *>(hb_smem));
+    } else {
+        for (int i = threadIdx.x; i < N; i += HB_T) env[i] = stage[i];
+        STAMP(11);
     }
     __syncthreads();
     STAMP(7);

@@ -7,6 +7,7 @@
  * prints the largest envelope differences (relative to max |env|).
  */
 #define BPMX_STAMPS 1
+#define BPMX_QS_STAMPS 1
 #include "../bpm_analysis_amd/csrc/k_hilbert.hip"
 
 #include <cstdio>
@@ -35,6 +36,12 @@ static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> 
     CK(hipMemcpy(da, act.data(), F * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dt, tabs.data(), tabs.size() * 16, hipMemcpyHostToDevice));
     HilbArgs a{dy, dd, da, 0, F, dt, denv, dst};
+    double *dqv = nullptr;
+    if (getenv("HB_Q")) {                       /* the library's one native-mode level (q = 0.1) */
+        CK(hipMalloc(&dqv, (size_t)F * Q_SLOTS * 8));
+        a.q.env = denv; a.q.doff = dd; a.q.active = da; a.q.n_files = F; a.q.qv = dqv;
+        a.q.n_levels = 1; a.q.q[0] = 0.1; a.q.slot[0] = 1; a.q.skip_le = QR_MAX;
+    }
     CK(hipFuncSetAttribute((const void *)k_hilbert_env, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -52,15 +59,25 @@ static double run(int F, int64_t nd, bool mfma, bool rader, std::vector<double> 
     CK(hipMemcpy(st.data(), dst, st.size() * 8, hipMemcpyDeviceToHost));
     env_out.resize(y.size());
     CK(hipMemcpy(env_out.data(), denv, y.size() * 8, hipMemcpyDeviceToHost));
-    double acc[11] = {0};
-    for (int f = 0; f < F; ++f) for (int k = 0; k < 11; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
+    if (dqv) {
+        std::vector<unsigned long long> qs((size_t)8 * 4096);
+        CK(hipMemcpyFromSymbol(qs.data(), HIP_SYMBOL(qs_dbg), qs.size() * 8));
+        double qa[8] = {0};
+        const int nf = F < 4096 ? F : 4096;
+        for (int f = 0; f < nf; ++f) for (int k = 0; k < 8; ++k) qa[k] += (double)qs[(size_t)f * 8 + k] / nf;
+        printf("select phases (cycles): vary %.0f hist0 %.0f digit-hist %.0f scan %.0f gather %.0f final %.0f\n",
+               qa[0], qa[1], qa[2], qa[3], qa[4], qa[5]);
+    }
+    double acc[12] = {0};
+    for (int f = 0; f < F; ++f) for (int k = 0; k < 12; ++k) acc[k] += (double)st[(size_t)f * 16 + k];
     printf("kernel %.4f ms;  mean cycles per workgroup (s_memtime):", ms / R);
-    const char *nm[11] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "store", "rollsum", "rm:barrier", "stage"};
+    const char *nm[12] = {"load", "fwd0", "fwd1", "fwd2", "pointwise", "inverse", "mag", "quantiles", "rollsum", "rm:barrier", "stage", "store"};
     double tot = 0;
-    for (int k = 0; k < 11; ++k) tot += acc[k] / F;
-    for (int k = 0; k < 11; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
+    for (int k = 0; k < 12; ++k) tot += acc[k] / F;
+    for (int k = 0; k < 12; ++k) printf(" %s %.0f (%.1f%%)", nm[k], acc[k] / F, 100.0 * acc[k] / F / tot);
     printf("\n");
     CK(hipFree(dy)); CK(hipFree(denv)); CK(hipFree(dd)); CK(hipFree(da)); CK(hipFree(dt)); CK(hipFree(dst));
+    if (dqv) CK(hipFree(dqv));
     return ms / R;
 }
 
