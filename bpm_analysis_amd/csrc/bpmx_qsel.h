@@ -14,6 +14,8 @@
 #ifndef BPMX_QSEL_H
 #define BPMX_QSEL_H
 
+#include <type_traits>
+
 #include "bpmx_common.h"
 #include "bpmx_kernels.h"
 
@@ -53,18 +55,19 @@ struct alignas(16) QrShared {
     long long cnt[QR_T / 64];
 };
 
-/* adds the wave's digits (dg < 0: none) to its own histogram row h with one
- * LDS atomic per run of equal digits over consecutive lanes (item it of the 64
- * lanes is 64 consecutive positions of a smooth envelope: a few runs).  A
- * uniform-digit fast path (one atomic of the ballot's count) measured slower.
- * Every lane must be active. */
+/* adds the wave's digits (dg < 0: none) to its own histogram row h.  A run
+ * [s, e] of equal digits over consecutive lanes adds e + 1 - s as -s at its
+ * first lane and e + 1 at its last (one atomic per lane that starts or ends a
+ * run, none for the lanes inside; the row's sums are exact mod 2^32).  Item it
+ * of the 64 lanes is 64 consecutive positions of a smooth envelope, so a wave
+ * has a few runs per item.  No lane-mask arithmetic: two DPP moves, two
+ * compares, one subtract.  Every lane must be active. */
 __device__ __forceinline__ void qr_hist_add(unsigned int *h, int dg) {
     const int lane = lane_id();
-    const int prev = wave_shr1_dpp(dg, -2);                  /* lane 0: -2, never a digit or -1 */
-    const uint64_t bm = __ballot(prev != dg);                /* run starts */
-    const uint64_t after = bm & ~((2ull << lane) - 1ull);
-    const int nxt = after ? __ffsll((long long)after) - 1 : 64;
-    if (dg >= 0 && ((bm >> lane) & 1ull)) atomicAdd(&h[dg], (unsigned int)(nxt - lane));
+    const int prev = __builtin_amdgcn_update_dpp(-2, dg, 0x138, 0xf, 0xf, false);   /* wave_shr:1, lane 0: -2 */
+    const int next = __builtin_amdgcn_update_dpp(-2, dg, 0x130, 0xf, 0xf, false);   /* wave_shl:1, lane 63: -2 */
+    const bool st = prev != dg, en = next != dg;
+    if (dg >= 0 && (st || en)) atomicAdd(&h[dg], (unsigned int)((en ? lane + 1 : 0) - (st ? lane : 0)));
 }
 
 /* wave-wide OR / AND / unsigned min of a 64-bit value by DPP row shifts and
