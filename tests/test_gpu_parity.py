@@ -930,11 +930,13 @@ def test_run_sharded_single_rank_on_the_gpu(det, tmp_path):
 
 @pytest.mark.gpu
 def test_quantile_kernel_paths(det):
-    """k_quantile_reg: the bin-gather fast path, its radix-select fallback (a
-    bin with more than 512 keys: long runs of tied values), a constant
-    envelope (no varying key bit) and the q = 0 / 1 ends, through the static
-    noise floor of envelopes without troughs (floor = np.quantile(env, q),
-    bpm_analysis.py:1075) and against the oracle's troughs and peaks."""
+    """qr_select (bpmx_qsel.h, in k_floor_wm's static floor and
+    k_quantile_reg): the gather once <= 64 keys share the prefix, long runs of
+    tied values (no bin ever that small), a constant envelope (no varying key
+    bit), the q = 0 / 1 ends and the (r+1)-th order statistic above the
+    gathered keys, through the static noise floor of envelopes without troughs
+    (floor = np.quantile(env, q), bpm_analysis.py:1075) and against the
+    oracle's troughs and peaks."""
     from bpm_analysis_amd import _native as N
     rng = np.random.default_rng(11)
     n = 18124
@@ -952,6 +954,21 @@ def test_quantile_kernel_paths(det):
         for (name, env), r in zip(envs.items(), got):
             want = np.quantile(env, q)
             assert np.all(r["floor"] == want), (name, q, r["floor"][:3], want)
+    # the select's (r+1)-th order statistic outside the keys it gathered: r
+    # the last key of its 16-bit key prefix on a wide-range envelope, and a
+    # step (r + 1 equal values, then a jump) where no bin ever drops to 64 keys
+    wide = envs["wide_range"]
+    top16 = (wide.view(np.uint64) ^ np.uint64(1 << 63)) >> np.uint64(48)
+    edges = np.flatnonzero(top16[1:] != top16[:-1])
+    for r in (int(edges[len(edges) // 5]), int(edges[len(edges) // 2]), int(edges[-2])):
+        q = (r + 0.5) / (n - 1)
+        params = dict(G.BASE_PARAMS)
+        params["noise_floor_quantile"] = q
+        step = np.where(np.arange(n) <= r, 1.0, 1.0e6)
+        got = det.run_env_host([wide, step], 302, params, N.STAGE_FLOOR)
+        for env, res in zip((wide, step), got):
+            want = np.quantile(env, q)
+            assert np.all(res["floor"] == want), (r, q, res["floor"][:3], want)
     # the prominence quantiles (0.1 of the envelope) on bumpy envelopes
     params = dict(G.BASE_PARAMS)
     t = np.arange(n)
