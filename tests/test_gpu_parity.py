@@ -566,6 +566,17 @@ def test_find_peaks_kernels_agree(det):
         assert _same(a[k]["peaks"], opk)
         assert a[k]["flags"] == ofl | (O.F_PEAK_TIE if ptie else 0)
     assert a[2]["flags"] & TIE_BITS
+    # a tied recording beyond 65536 samples through engine.resolve_ties (the
+    # ordered sub-batch takes the single-workgroup k_find_peaks with the run's
+    # own options forwarded), beside a tied short one: numpy's order exactly
+    for opt in (0, N.OPT_PEAKS_GLOBAL):
+        pair = [long_envs[2], envs[-3]]
+        rs = det.run_env_host(pair, 302, params, stages, options=opt, resolve_ties=True)
+        for e, r in zip(pair, rs):
+            nf, nt, nfl, nraw, npk = _numpy_order_answer(e, d, params)
+            assert _same(r["troughs"], nt) and _same(r["floor"], nf) and _same(r["peaks"], npk)
+            assert r["n_raw_troughs"] == len(nraw)
+            assert r["flags"] & TIE_BITS == 0
 
 
 @pytest.mark.parametrize("fs", [44100, 22050, 48000])
