@@ -332,7 +332,11 @@ __device__ __forceinline__ void hb_radixp_mfma(const HbLds &S, const HilbPlan &P
     }
     __syncthreads();
     const int ntl = (h + 16) >> 4, ks = (h + 3) >> 2, units = ((nbf + 15) >> 4) * ntl;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
+    /* thread-derived values recomputed here from an opaque copy: hoisted to
+     * the kernel's entry they stayed live across every stage and spilled */
+    int tx = (int)threadIdx.x;
+    asm volatile("" : "+v"(tx));
+    const int lane = tx & 63, wv = __builtin_amdgcn_readfirstlane(tx >> 6), r16 = lane & 15, kq = lane >> 4;
     auto base_of = [&](int bf) {
         if (CONTIG) return bf * p;
         const int blk = hb_div(bf, dL);
