@@ -271,7 +271,11 @@ __device__ __forceinline__ void qr_select(const uint64_t (&key)[QR_IT], int64_t 
             }
             res = np_lerp(va, key_f64(kb), vi - (double)lo);
         }
-        if (tid < Q_SLOTS && ((A.slot[l] >> tid) & 1)) A.qv[(int64_t)f * Q_SLOTS + tid] = res;
+        {
+            int ts = tid;                                    /* the store address formed here, not hoisted and spilled */
+            asm volatile("" : "+v"(ts));
+            if (ts < Q_SLOTS && ((A.slot[l] >> ts) & 1)) A.qv[(int64_t)f * Q_SLOTS + ts] = res;
+        }
         __syncthreads();
         QS_T(5);
     }
