@@ -55,7 +55,22 @@ struct HilbArgs {
     double *env;
     unsigned long long *stamps;    /* tools/hbench phase timing only (nullptr) */
     QuantArgs q;                   /* q.n_levels > 0: also the recording's quantiles (qr_select) into q.qv */
+    /* fy != 0: yd of the full decimation tiles (bt blocks each) made here from
+     * k_native_blocks' gamma rows and k_native_carry's tile carries, with
+     * k_native_yd's arithmetic (yd_j = alpha_b . Qe_t + beta_b . S0_t +
+     * gamma_j), straight into the FFT buffer and into ys for the magnitude
+     * pass's second read; the rest of yd (partial tile, tail) comes from
+     * k_native_carry's writes to yd */
+    int32_t fy;
+    int32_t bt, gstr;              /* blocks per tile (even, <= 64); gamma row stride */
+    const double *gam;             /* [tile][gstr] */
+    const double *car;             /* [tile][8]: S0_t | Qe_t */
+    const double *al, *be;         /* [64][4] each: alpha_b, beta_b */
+    const int64_t *toff;           /* [F] first tile of recording f */
+    double *ys;                    /* recording f's full-tile yd at hb_ys_off(doff[f], f): 128-byte aligned,
+                                    * no cache line shared with another recording */
 };
+__host__ __device__ inline int64_t hb_ys_off(int64_t d0, int64_t f) { return ((d0 + 15) & ~(int64_t)15) + 16 * f; }
 
 __global__ void k_hilbert_env(HilbArgs A, HilbPlan P);
 

@@ -2183,7 +2183,24 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.ttab = carry_serial ? nullptr : d_tt2;
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
     }
-    if (nt > 0) {
+    /* k_hilbert_env makes yd of the full tiles itself (HilbArgs::fy) when every
+     * active recording takes it, the tiles hold an even number of blocks and
+     * yd is not an output: then k_native_yd's launch and its yd write go away */
+    static const bool no_fy = std::getenv("BPMX_NO_FY") != nullptr;   /* A/B diagnostic, read once */
+    bool fy = !O->y && bt % 2 == 0 && bt <= 64 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) && !no_fy;
+    for (int f0 = 0; fy && f0 < F;) {
+        const int64_t nd = doff[f0 + 1] - doff[f0];
+        int f1 = f0 + 1;
+        while (f1 < F && doff[f1 + 1] - doff[f1] == nd) ++f1;
+        HilbPlan hp;
+        size_t hlds = 0;
+        if (nd > 15 && hb_tables(ctx, nd, P->env_window, &hp, &hlds, s, &rc) == nullptr) fy = false;
+        if (rc != BPMX_OK) return rc;
+        f0 = f1;
+    }
+    double *ys = fy ? (double *)ctx->buf("nat_ys", (size_t)(doff[F] + 32 * (int64_t)F + 16) * 8, &rc) : nullptr;
+    if (rc != BPMX_OK) return rc;
+    if (nt > 0 && !fy) {
         NatYdArgs a;
         a.tiles = d_tiles; a.bt = bt; a.tt = d_tt; a.carry = carry; a.gam = gam; a.yd = yd;
         LAUNCH(ctx, s, "k_native_yd", k_native_yd, dim3((unsigned)nt), dim3(64), 0, s, a);
@@ -2213,6 +2230,9 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 HilbArgs a;
                 a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
                 a.tabs = ht->dev; a.env = O->env; a.stamps = nullptr;
+                a.fy = fy ? 1 : 0; a.bt = bt; a.gstr = (int32_t)gstr; a.gam = gam; a.car = carry;
+                a.al = d_tt + TT_ALPHA; a.be = d_tt + TT_BETA;
+                a.toff = d_geo + F + 1; a.ys = ys;
                 a.q = QuantArgs{};
                 if (qa) {
                     a.q = *qa;                                   /* the select's scratch is the stage region */

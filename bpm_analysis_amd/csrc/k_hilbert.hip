@@ -560,6 +560,9 @@ __device__ __forceinline__ int hb_pos(const HilbPlan &P, int k) {     /* positio
 }
 
 static_assert(HB_T == QR_T, "k_hilbert_env runs qr_select with its own threads");
+#ifndef BPMX_HB_YT
+#define BPMX_HB_YT 8   /* fused yd: tiles per wave per round trip (8, 16, 24 measured alike; 24 spilled SGPRs) */
+#endif
 
 __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     const int f = A.f_begin + blockIdx.x;
@@ -586,13 +589,69 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
     const bool r2 = P.rad[0] == 2 && P.B[0] == M;
     const int H = M / 2;
     for (int i = threadIdx.x; i < P.ntwh + 128 + P.nptab + P.nrtab; i += HB_T) S.twh[i] = A.tabs[i];
-    if (!r2)
+    const bool fy = A.fy != 0;
+    if (fy) {
+        /* yd of the full tiles, one tile per wave step (lane = block b): the
+         * tile's carries by one scalar load, gamma by one coalesced row read;
+         * the real array y fills S.x as the complex pairs the transform packs */
+        double *xr = (double *)S.x;
+        double *ydw = A.ys + hb_ys_off(d0, f);
+        const int lane = (int)(threadIdx.x & 63), wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int64_t tf0 = A.toff[f];
+        const int btv = A.bt, ntf = (N - 1) / btv;             /* full tiles: (Nd - 1) / bt */
+        const bool on = lane < btv;
+        double al[4], be[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { al[k] = on ? A.al[4 * lane + k] : 0.0; be[k] = on ? A.be[4 * lane + k] : 0.0; }
+        /* eight tiles per round trip: lane l loads carry word l % 8 of the
+         * round's tile l / 8 (one instruction for all eight), each tile's gamma
+         * row is one load, all issued before any use; a tile's carries then
+         * come out by readlane (wave-uniform) */
+        constexpr int HB_YT = BPMX_HB_YT, HB_YC = (HB_YT + 7) / 8;
+        for (int t0 = wv; t0 < ntf; t0 += HB_YT * (HB_T / 64)) {
+            double cvs[HB_YC];
+#pragma unroll
+            for (int q = 0; q < HB_YC; ++q) {
+                const int tl = t0 + (8 * q + (lane >> 3)) * (HB_T / 64);
+                cvs[q] = tl < ntf ? A.car[(tf0 + tl) * 8 + (lane & 7)] : 0.0;
+            }
+            double g[HB_YT];
+#pragma unroll
+            for (int u = 0; u < HB_YT; ++u) {
+                const int tt = t0 + u * (HB_T / 64);
+                g[u] = (on && tt < ntf) ? __builtin_nontemporal_load(A.gam + (tf0 + tt) * A.gstr + lane) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < HB_YT; ++u) {
+                const int tt = t0 + u * (HB_T / 64);
+                if (tt >= ntf) break;                          /* uniform */
+                double c[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const double cv = cvs[u / 8];
+                    const int lo = __builtin_amdgcn_readlane(__double2loint(cv), 8 * (u % 8) + k);
+                    const int hi = __builtin_amdgcn_readlane(__double2hiint(cv), 8 * (u % 8) + k);
+                    c[k] = __hiloint2double(hi, lo);
+                }
+                if (on) {
+                    const double ya = __builtin_fma(al[0], c[4], __builtin_fma(al[1], c[5], __builtin_fma(al[2], c[6], al[3] * c[7])));
+                    const double yb = __builtin_fma(be[0], c[0], __builtin_fma(be[1], c[1], __builtin_fma(be[2], c[2], be[3] * c[3])));
+                    const double y = ya + yb + g[u];
+                    const int j = tt * btv + lane;
+                    xr[j] = y;
+                    ydw[j] = y;
+                }
+            }
+        }
+        for (int j = ntf * btv + (int)threadIdx.x; j < N; j += HB_T) xr[j] = y1[j];   /* k_native_carry's part */
+    } else if (!r2) {
         for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = y2(m);
+    }
     __syncthreads();
     STAMP_DECL
     if (r2) {
         for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIF radix 2: L = M / 2, twiddle W_N^(2t) */
-            const double2 a = y2(t), b = y2(t + H), d = csub(a, b);
+            const double2 a = fy ? S.x[t] : y2(t), b = fy ? S.x[t + H] : y2(t + H), d = csub(a, b);
             S.x[t] = cadd(a, b);
             S.x[t + H] = t ? cmul(d, S.tw(2 * t)) : d;
         }
@@ -643,9 +702,19 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
         const double i0 = c.x * inv, i1 = c.y * inv;
         return make_double2(sqrt(y.x * y.x + i0 * i0), sqrt(y.y * y.y + i1 * i1));
     };
+    /* y for |analytic|: the full tiles' pairs from ys (written by this
+     * workgroup's first phase: every wave's stores complete, then a barrier),
+     * the rest from yd */
+    const int jfy = fy ? (N - 1) / A.bt * A.bt : 0;           /* even: bt is */
+    const double2 *ys2 = fy ? (const double2 *)(A.ys + hb_ys_off(d0, f)) : nullptr;
+    if (fy) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    auto ym = [&](int m) -> double2 { return 2 * m < jfy ? ys2[m] : y2(m); };
     if (r2) {
         for (int t = threadIdx.x; t < H; t += HB_T) {        /* DIT radix 2 (conjugate twiddle before), then |.| */
-            const double2 ya = y2(t), yb = y2(t + H);
+            const double2 ya = ym(t), yb = ym(t + H);
             const double2 a = S.x[t];
             double2 b = S.x[t + H];
             if (t) b = cmulc(b, S.tw(2 * t));
@@ -653,7 +722,7 @@ __global__ __launch_bounds__(HB_T) void k_hilbert_env(HilbArgs A, HilbPlan P) {
             S.x[t + H] = mag2(csub(a, b), yb);
         }
     } else {
-        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = mag2(S.x[m], y2(m));
+        for (int m = threadIdx.x; m < M; m += HB_T) S.x[m] = mag2(S.x[m], ym(m));
     }
     __syncthreads();
     STAMP(6);

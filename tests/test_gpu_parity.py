@@ -1340,6 +1340,27 @@ def test_batch_pipeline_identical(det, mode):
                 assert _same(a[k], b[k]), k
 
 
+@pytest.mark.gpu
+def test_native_fused_yd_identical(det):
+    """k_hilbert_env making yd of the full decimation tiles itself (HilbArgs::fy:
+    no y output requested, every recording on the fused Hilbert plan) gives the
+    same env, floor, troughs, peaks and flags bit for bit as k_native_yd
+    followed by the kernel (y requested), on a ragged batch with odd decimated
+    offsets, partial last tiles and a recording shorter than one tile."""
+    from bpm_analysis_amd import _native as N
+    fs = 44100
+    lens = [fs * 11 + 3, fs * 6 + 1, 146 * 40 + 7, fs * 9, fs * 60]
+    fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    params = dict(G.BASE_PARAMS)
+    pcm = det.synth(fo, fs, 1, seed0=314)
+    fused = det.run(pcm, fo, fs, params, mode="native").to_host()
+    plain = det.run(pcm, fo, fs, params, mode="native", want_y=True).to_host()
+    for a, b in zip(fused, plain):
+        for k in ("env", "floor", "troughs", "peaks"):
+            assert _same(a[k], b[k]), k
+        assert a["flags"] == b["flags"]
+
+
 def test_native_envelope_independent_of_placement(det):
     """A recording's native envelope (and everything after it) is bit-identical
     wherever its PCM lies: a batch started 1..8 frames into an aligned buffer
