@@ -171,7 +171,10 @@ typedef struct {
 typedef struct {
     double *env;        /* f64 envelope */
     double *floor;      /* f64 dynamic noise floor */
-    double *y;          /* optional (NULL): filtered decimated signal (debug WAV, :1047-1060) */
+    double *y;          /* optional (NULL): filtered decimated signal (debug WAV, :1047-1060).
+                         * Native mode: asking for it keeps a separate yd pass (~0.05 ms per
+                         * 1024 x 60 s batch on MI355X); left NULL, the envelope kernel makes
+                         * yd itself. */
     int64_t *troughs;   /* sanitised trough indices, per-file slice, n_troughs[f] valid */
     int64_t *peaks;     /* raw peak indices, per-file slice, n_peaks[f] valid */
     int32_t *n_troughs; /* [n_files] */
