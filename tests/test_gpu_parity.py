@@ -1347,14 +1347,24 @@ def test_native_fused_yd_identical(det):
     same env, floor, troughs, peaks and flags bit for bit as k_native_yd
     followed by the kernel (y requested), on a ragged batch with odd decimated
     offsets, partial last tiles and a recording shorter than one tile."""
-    from bpm_analysis_amd import _native as N
-    fs = 44100
-    lens = [fs * 11 + 3, fs * 6 + 1, 146 * 40 + 7, fs * 9, fs * 60]
+    fs = 44100                                       # ds = 146: Nd = ceil(n / 146), 62-block tiles
+    # even Nd for every recording (an odd Nd takes another transform, and the
+    # whole batch the unfused path): 3322 / 1800 (odd decimated offsets after
+    # the first) / 58 (shorter than one tile) / 18124 samples
+    lens = [146 * 3322 - 5, 146 * 1800, 146 * 58 - 1, 146 * 18124 - 77]
     fo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     params = dict(G.BASE_PARAMS)
     pcm = det.synth(fo, fs, 1, seed0=314)
+    det.profile_only("")
+    det.profile(True)
     fused = det.run(pcm, fo, fs, params, mode="native").to_host()
+    det.profile(False)
+    assert "k_native_yd" not in det.profile_read()       # yd made inside k_hilbert_env
+    det.profile(True)
     plain = det.run(pcm, fo, fs, params, mode="native", want_y=True).to_host()
+    det.profile(False)
+    assert "k_native_yd" in det.profile_read()
+    assert [r["env"].size for r in plain] == [3322, 1800, 58, 18124]
     for a, b in zip(fused, plain):
         for k in ("env", "floor", "troughs", "peaks"):
             assert _same(a[k], b[k]), k
