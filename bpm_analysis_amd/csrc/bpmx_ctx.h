@@ -43,6 +43,7 @@ struct bpmx_ctx {
     std::vector<int64_t> blu_key;     /* Bluestein group geometry of the FFT(b) tables in "blu_b" */
     std::vector<int32_t> blu_files;   /* host copy of the Bluestein groups' file lists */
     std::vector<int32_t> nat_fused;   /* per-file: envelope done by the fused Hilbert kernel (host copy outlives async uploads) */
+    std::vector<int32_t> nat_fyrec;   /* per-file: yd made inside k_hilbert_env (k_native_yd skips its tiles) */
     std::vector<int64_t> nat_boff;              /* block offsets | per-file tile offsets */
     std::vector<int64_t> nat_tkey;              /* tile-list geometry key */
     std::vector<char> nat_tiles;                /* host copy of the tile list */

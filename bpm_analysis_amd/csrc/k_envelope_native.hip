@@ -114,6 +114,7 @@ constexpr int NAT_TT_ROWS = NAT_DSMAX + 20, NAT_TT_PAR = 320;
 
 struct NatYdArgs {
     const NatTile *tiles;
+    const int32_t *skip;            /* [F] optional: recordings whose yd k_hilbert_env makes */
     int32_t bt;
     const double *tt, *carry, *gam;
     double *yd;
@@ -1419,6 +1420,7 @@ __global__ __launch_bounds__(64) void k_native_yd(NatYdArgs A) {
     const NatTile tl = nat_tile_ld(A.tiles, t);
     const int bt = A.bt, lane = threadIdx.x;
     if (tl.nb - tl.j0 < bt || lane >= bt) return;          /* partial tiles: k_native_carry */
+    if (A.skip && A.skip[tl.f]) return;                    /* uniform: yd made by k_hilbert_env */
     const double *c = A.carry + t * 8;
     const V4 S0 = nat_ld4(c), Qe = nat_ld4(c + 4);
     const V4 al = nat_ld4(A.tt + TT_ALPHA + 4 * lane), be = nat_ld4(A.tt + TT_BETA + 4 * lane);
@@ -2183,26 +2185,38 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
         a.ttab = carry_serial ? nullptr : d_tt2;
         LAUNCH(ctx, s, "k_native_carry", k_native_carry, dim3(F), dim3(64), 0, s, a, ss);
     }
-    /* k_hilbert_env makes yd of the full tiles itself (HilbArgs::fy) when every
-     * active recording takes it, the tiles hold an even number of blocks and
-     * yd is not an output: then k_native_yd's launch and its yd write go away */
+    /* k_hilbert_env makes yd of the full tiles itself (HilbArgs::fy) for every
+     * run of recordings it takes, when the tiles hold an even number of blocks
+     * and yd is not an output; k_native_yd then covers only the other
+     * recordings' tiles (a skip list), and is not launched when none is left */
     static const bool no_fy = std::getenv("BPMX_NO_FY") != nullptr;   /* A/B diagnostic, read once */
-    bool fy = !O->y && bt % 2 == 0 && bt <= 64 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) && !no_fy;
-    for (int f0 = 0; fy && f0 < F;) {
+    const bool fy_ok = !O->y && bt % 2 == 0 && bt <= 64 && !(P->options & BPMX_OPT_HILBERT_ROCFFT) && !no_fy;
+    std::vector<int32_t> &fyrec = ctx->nat_fyrec;
+    fyrec.assign(F, 0);
+    bool any_fy = false, all_fy = true;
+    for (int f0 = 0; f0 < F;) {
         const int64_t nd = doff[f0 + 1] - doff[f0];
         int f1 = f0 + 1;
         while (f1 < F && doff[f1 + 1] - doff[f1] == nd) ++f1;
-        HilbPlan hp;
-        size_t hlds = 0;
-        if (nd > 15 && hb_tables(ctx, nd, P->env_window, &hp, &hlds, s, &rc) == nullptr) fy = false;
-        if (rc != BPMX_OK) return rc;
+        if (nd > 15) {
+            HilbPlan hp;
+            size_t hlds = 0;
+            const bool plan = fy_ok && hb_tables(ctx, nd, P->env_window, &hp, &hlds, s, &rc) != nullptr;
+            if (rc != BPMX_OK) return rc;
+            for (int f = f0; f < f1; ++f) fyrec[f] = plan ? 1 : 0;
+            any_fy |= plan;
+            all_fy &= plan;
+        }
         f0 = f1;
     }
-    double *ys = fy ? (double *)ctx->buf("nat_ys", (size_t)(doff[F] + 32 * (int64_t)F + 16) * 8, &rc) : nullptr;
+    double *ys = any_fy ? (double *)ctx->buf("nat_ys", (size_t)(doff[F] + 32 * (int64_t)F + 16) * 8, &rc) : nullptr;
+    int32_t *d_fyrec = any_fy ? (int32_t *)ctx->buf("nat_fyrec", (size_t)F * 4, &rc) : nullptr;
     if (rc != BPMX_OK) return rc;
-    if (nt > 0 && !fy) {
+    if (any_fy && !all_fy) HIP_TRY(hipMemcpyAsync(d_fyrec, fyrec.data(), (size_t)F * 4, hipMemcpyHostToDevice, s));
+    if (nt > 0 && !all_fy) {
         NatYdArgs a;
-        a.tiles = d_tiles; a.bt = bt; a.tt = d_tt; a.carry = carry; a.gam = gam; a.yd = yd;
+        a.tiles = d_tiles; a.skip = any_fy ? d_fyrec : nullptr; a.bt = bt; a.tt = d_tt; a.carry = carry; a.gam = gam;
+        a.yd = yd;
         LAUNCH(ctx, s, "k_native_yd", k_native_yd, dim3((unsigned)nt), dim3(64), 0, s, a);
     }
     /* Hilbert + envelope: runs of equal Nd share a plan.  The fused LDS kernel
@@ -2230,7 +2244,7 @@ int native_envelope(bpmx_ctx *ctx, const bpmx_params *P, const bpmx_batch *B, co
                 HilbArgs a;
                 a.yd = yd; a.doff = d_doff; a.active = d_active; a.f_begin = f0; a.f_end = f1;
                 a.tabs = ht->dev; a.env = O->env; a.stamps = nullptr;
-                a.fy = fy ? 1 : 0; a.bt = bt; a.gstr = (int32_t)gstr; a.gam = gam; a.car = carry;
+                a.fy = fyrec[f0]; a.bt = bt; a.gstr = (int32_t)gstr; a.gam = gam; a.car = carry;
                 a.al = d_tt + TT_ALPHA; a.be = d_tt + TT_BETA;
                 a.toff = d_geo + F + 1; a.ys = ys;
                 a.q = QuantArgs{};

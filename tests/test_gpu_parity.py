@@ -1346,7 +1346,8 @@ def test_native_fused_yd_identical(det):
     no y output requested, every recording on the fused Hilbert plan) gives the
     same env, floor, troughs, peaks and flags bit for bit as k_native_yd
     followed by the kernel (y requested), on a ragged batch with odd decimated
-    offsets, partial last tiles and a recording shorter than one tile."""
+    offsets, partial last tiles and a recording shorter than one tile, and on
+    a ragged batch mixing fused (even Nd) and unfused (odd Nd) recordings."""
     fs = 44100                                       # ds = 146: Nd = ceil(n / 146), 62-block tiles
     # even Nd for every recording (an odd Nd takes another transform, and the
     # whole batch the unfused path): 3322 / 1800 (odd decimated offsets after
@@ -1366,6 +1367,21 @@ def test_native_fused_yd_identical(det):
     assert "k_native_yd" in det.profile_read()
     assert [r["env"].size for r in plain] == [3322, 1800, 58, 18124]
     for a, b in zip(fused, plain):
+        for k in ("env", "floor", "troughs", "peaks"):
+            assert _same(a[k], b[k]), k
+        assert a["flags"] == b["flags"]
+    # a ragged batch mixing odd Nd (another transform, yd from k_native_yd,
+    # which skips the fused recordings' tiles) with even Nd (fused)
+    lens2 = [146 * 3321 - 9, 146 * 1800, 146 * 2401, 146 * 58 - 1, 146 * 5000 - 3]
+    fo2 = np.concatenate([[0], np.cumsum(lens2)]).astype(np.int64)
+    pcm2 = det.synth(fo2, fs, 1, seed0=2718)
+    det.profile(True)
+    mixed = det.run(pcm2, fo2, fs, params, mode="native").to_host()
+    det.profile(False)
+    assert "k_native_yd" in det.profile_read()
+    plain2 = det.run(pcm2, fo2, fs, params, mode="native", want_y=True).to_host()
+    assert [r["env"].size % 2 for r in plain2] == [1, 0, 1, 0, 0]
+    for a, b in zip(mixed, plain2):
         for k in ("env", "floor", "troughs", "peaks"):
             assert _same(a[k], b[k]), k
         assert a["flags"] == b["flags"]
